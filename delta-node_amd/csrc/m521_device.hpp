@@ -1,0 +1,206 @@
+// m521_device.hpp — in-lane multi-limb arithmetic mod p = 2^521 - 1 (gfx950).
+//
+// One field element per lane, 17 little-endian u32 limbs held in VGPRs.
+// Values are kept "lazy" (any integer < 2^544 that fits the 17 limbs) between
+// operations and brought to the canonical residue in [0, p) only before a
+// store, using the Mersenne identity 2^521 == 1 (mod p): reduction is a
+// shift + add (fold), never a division.  This restates the `% prime` steps of
+// the reference's `_eval_at` (delta_node/crypto/shamir/shamir.py:19-25) and
+// the `% self.prime` / `div_mod` of `resolve_shares` (shamir.py:86-90).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dn {
+
+constexpr int kLimbs = 17;
+constexpr uint32_t kTopMask = 0x1FFu;  // bits 512..520 live in limb 16
+constexpr int kTile = 256;             // elements per layout tile
+constexpr uint64_t kTileBytes = 66ull * kTile;
+constexpr uint64_t kHiOffset = 64ull * kTile;  // byte offset of the u16 plane
+
+// ---- tiled-layout addressing (see include/dn_shamir.h) --------------------
+// Every wave works on one tile at a time, so the tile base is wave-uniform
+// (SGPRs) and each lane only adds a 32-bit offset: the loads/stores below
+// compile to the saddr form `global_load_dword v, v_off, s[base:base+1] offset:imm`,
+// which keeps per-limb 64-bit addresses out of the VGPR budget.
+__device__ __forceinline__ const uint8_t* tile_base(const uint8_t* vec, uint32_t tile) {
+  return vec + static_cast<uint64_t>(tile) * kTileBytes;
+}
+__device__ __forceinline__ uint8_t* tile_base(uint8_t* vec, uint32_t tile) {
+  return vec + static_cast<uint64_t>(tile) * kTileBytes;
+}
+
+// Byte offsets are formed as u32 (w < 256) and added to a uniform per-limb
+// pointer so that the compiler can use SGPR-base + VGPR-offset addressing.
+template <typename T>
+__device__ __forceinline__ const T* at(const uint8_t* base, uint32_t byte_off) {
+  return reinterpret_cast<const T*>(base + byte_off);
+}
+template <typename T>
+__device__ __forceinline__ T* at(uint8_t* base, uint32_t byte_off) {
+  return reinterpret_cast<T*>(base + byte_off);
+}
+
+// Load element w (0..255) of the tile at `tb`.  The top limb is masked to 9 bits.
+__device__ __forceinline__ void load_fe(const uint8_t* __restrict__ tb, uint32_t w, uint32_t v[kLimbs]) {
+  const uint32_t o4 = w * 4u, o2 = w * 2u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = __builtin_nontemporal_load(at<uint32_t>(tb + i * 4 * kTile, o4));
+  v[16] = static_cast<uint32_t>(__builtin_nontemporal_load(at<uint16_t>(tb + kHiOffset, o2))) & kTopMask;
+}
+
+// Same, through the caches (data re-read by the generic split kernel).
+__device__ __forceinline__ void load_fe_cached(const uint8_t* __restrict__ tb, uint32_t w, uint32_t v[kLimbs]) {
+  const uint32_t o4 = w * 4u, o2 = w * 2u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = *at<uint32_t>(tb + i * 4 * kTile, o4);
+  v[16] = static_cast<uint32_t>(*at<uint16_t>(tb + kHiOffset, o2)) & kTopMask;
+}
+
+// Store a canonical element (write-once data: non-temporal stores).
+__device__ __forceinline__ void store_fe(uint8_t* __restrict__ tb, uint32_t w, const uint32_t v[kLimbs]) {
+  const uint32_t o4 = w * 4u, o2 = w * 2u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) __builtin_nontemporal_store(v[i], at<uint32_t>(tb + i * 4 * kTile, o4));
+  __builtin_nontemporal_store(static_cast<uint16_t>(v[16]), at<uint16_t>(tb + kHiOffset, o2));
+}
+
+// ---- carry chains ----------------------------------------------------------
+// v += s (s a small u32), ripple through all limbs.
+__device__ __forceinline__ void add_small(uint32_t v[kLimbs], uint32_t s) {
+  unsigned c;
+  v[0] = __builtin_addc(v[0], s, 0u, &c);
+#pragma unroll
+  for (int i = 1; i < kLimbs; ++i) v[i] = __builtin_addc(v[i], 0u, c, &c);
+}
+
+// v (< 2^521 + 2^23) -> canonical residue in [0, p).
+//   top bit 521 set  => v - p = (v - 2^521) + 1, and v - 2^521 < 2^23 sits in limb 0;
+//   v == p (all 521 bits set) => 0 (a branch no lane takes in practice).
+__device__ __forceinline__ void canon(uint32_t v[kLimbs]) {
+  const uint32_t top = v[16] >> 9;
+  uint32_t a = v[0];
+#pragma unroll
+  for (int i = 1; i < 16; ++i) a &= v[i];
+  const bool is_p = (a == 0xFFFFFFFFu) && (v[16] == kTopMask);
+  v[16] &= kTopMask;
+  v[0] += top;
+  if (__builtin_expect(is_p, 0)) {
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) v[i] = 0u;
+  }
+}
+
+// Lazy v (< 2^544) -> canonical.  One fold (bits >= 521 added back at bit 0)
+// leaves v < 2^521 + 2^23, then canon().
+__device__ __forceinline__ void reduce(uint32_t v[kLimbs]) {
+  const uint32_t hi = v[16] >> 9;
+  v[16] &= kTopMask;
+  add_small(v, hi);
+  canon(v);
+}
+
+// Lazy fold only: v (< 2^544) -> v' == v (mod p), v' < 2^521 + 2^23.
+__device__ __forceinline__ void fold(uint32_t v[kLimbs]) {
+  const uint32_t hi = v[16] >> 9;
+  v[16] &= kTopMask;
+  add_small(v, hi);
+}
+
+// v = src * x + c   (x < 2^16, caller guarantees the result < 2^544).
+// Product limbs come from a v_mad_u64_u32 chain whose 64-bit addend carries
+// only the previous high word; c is added by a separate v_addc chain.  (Folding
+// c into the mad addend makes hipcc hoist 17 zero-extended {c_i, 0} pairs out
+// of the share loop and doubles the register footprint.)
+__device__ __forceinline__ void mul_small_add(uint32_t v[kLimbs], const uint32_t src[kLimbs], uint32_t x,
+                                              const uint32_t c[kLimbs]) {
+  uint32_t hi = 0u;
+  unsigned cc = 0u;
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) {
+    const uint64_t t = static_cast<uint64_t>(src[i]) * x + hi;
+    hi = static_cast<uint32_t>(t >> 32);
+    v[i] = __builtin_addc(static_cast<uint32_t>(t), c[i], cc, &cc);
+  }
+}
+__device__ __forceinline__ void mul_small_add(uint32_t v[kLimbs], uint32_t x, const uint32_t c[kLimbs]) {
+  mul_small_add(v, v, x, c);
+}
+
+// ---- wide accumulators (reconstruct) --------------------------------------
+// S[0..N) += a[0..A) * y[0..17)   (schoolbook).  FRESH: S was zero before the
+// call, so limb j+17 is still untouched when row j ends and takes the carry
+// directly; otherwise each row's carry ripples to the top limb.
+template <int N, int A, bool FRESH = false>
+__device__ __forceinline__ void mac_wide(uint32_t S[N], const uint32_t* a, const uint32_t y[kLimbs]) {
+#pragma unroll
+  for (int j = 0; j < A; ++j) {
+    const uint32_t aj = a[j];
+    uint64_t carry = 0;
+#pragma unroll
+    for (int l = 0; l < kLimbs; ++l) {
+      const uint64_t t = static_cast<uint64_t>(aj) * y[l] + (static_cast<uint64_t>(S[j + l]) + carry);
+      S[j + l] = static_cast<uint32_t>(t);
+      carry = t >> 32;
+    }
+    if constexpr (FRESH) {
+      if (j + kLimbs < N) S[j + kLimbs] = static_cast<uint32_t>(carry);
+    } else {
+      unsigned c;
+      S[j + kLimbs] = __builtin_addc(S[j + kLimbs], static_cast<uint32_t>(carry), 0u, &c);
+#pragma unroll
+      for (int m = j + kLimbs + 1; m < N; ++m) S[m] = __builtin_addc(S[m], 0u, c, &c);
+    }
+  }
+}
+
+// N-limb S holding a value < 2^VALUE_BITS -> canonical 17-limb residue.
+// One fold r = (S mod 2^521) + (S >> 521); VALUE_BITS <= 1064 keeps S >> 521
+// below 2^543, so r < 2^544 fits 17 limbs (the limbs of S >> 521 beyond 17
+// are zero by the value bound), then reduce().
+template <int N, int VALUE_BITS>
+__device__ __forceinline__ void reduce_wide(const uint32_t S[N], uint32_t r[kLimbs]) {
+  static_assert(N > kLimbs && VALUE_BITS <= 32 * N && VALUE_BITS <= 1064, "reduce_wide bound");
+  constexpr int H = (VALUE_BITS - 521 + 31) / 32;  // limbs of S >> 521 that can be non-zero
+  static_assert(H <= kLimbs, "reduce_wide: high part wider than 17 limbs");
+  unsigned c = 0;
+#pragma unroll
+  for (int m = 0; m < kLimbs; ++m) {
+    uint32_t h = 0u;
+    if (m < H) {
+      h = S[16 + m] >> 9;
+      if (16 + m + 1 < N) h |= S[16 + m + 1] << 23;
+    }
+    const uint32_t lo = (m < 16) ? S[m] : (S[16] & kTopMask);
+    r[m] = __builtin_addc(lo, h, c, &c);
+  }
+  reduce(r);
+}
+
+// r = x * c mod p (c full width, uniform), canonical in and out.
+__device__ __forceinline__ void mulmod(uint32_t r[kLimbs], const uint32_t x[kLimbs], const uint32_t* c) {
+  uint32_t S[2 * kLimbs];
+#pragma unroll
+  for (int i = 0; i < 2 * kLimbs; ++i) S[i] = 0u;
+  mac_wide<2 * kLimbs, kLimbs, true>(S, c, x);
+  reduce_wide<2 * kLimbs, 1042>(S, r);
+}
+
+// x / 2^e mod p for canonical x, 1 <= e <= 31: a right rotation of the
+// 521-bit string (2^521 == 1), which keeps the result canonical.
+__device__ __forceinline__ void rotr521(uint32_t v[kLimbs], uint32_t e) {
+  const uint32_t low = v[0] & ((1u << e) - 1u);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = __builtin_amdgcn_alignbit(v[i + 1], v[i], e);
+  v[16] >>= e;
+  if (e <= 9) {
+    v[16] |= low << (9u - e);
+  } else {
+    v[15] |= low << (41u - e);
+    v[16] |= low >> (e - 9u);
+  }
+}
+
+}  // namespace dn

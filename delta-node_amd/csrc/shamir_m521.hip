@@ -1,0 +1,344 @@
+// shamir_m521.hip — split / reconstruct kernels for gfx950 and their C-ABI.
+//
+// Split (reference: SecretShare.make_shares, delta_node/crypto/shamir/shamir.py:55-66,
+// with _eval_at :19-25): per element, Horner evaluation of
+//   f(x) = c0 + c1 x + ... + c_{t-1} x^{t-1}  at x = 1..n, mod p = 2^521 - 1.
+// Reconstruct (reference: SecretShare.resolve_shares, shamir.py:68-90):
+//   f(0) = sum_i lambda_i y_i mod p over ALL k given shares.
+//
+// Mapping: one wave owns one 256-element layout tile at a time (grid-stride
+// over tiles); lane l handles tile elements l, l+64, l+128, l+192 in turn,
+// one element per lane, all 17 limbs in VGPRs.  Every global access of a
+// wave-instruction is one contiguous 256-byte (u32 plane) or 128-byte (u16
+// plane) run.  Inputs are read once and shares written once, so loads and
+// stores are non-temporal.  The path is HBM-bound: no MFMA (this is not a
+// contraction), only v_mad_u64_u32 / v_add_co chains in the VALU.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "dn_internal.hpp"
+#include "m521_device.hpp"
+
+namespace dn {
+
+struct SplitArgs {
+  const int64_t* sec_u64;  // int64 secrets (u64 two's-complement view), or null
+  const uint8_t* sec_fe;   // tiled field-element secrets, or null
+  const uint8_t* coeffs;   // block of t-1 tiled vectors
+  uint8_t* shares;         // block of n tiled vectors
+  uint64_t n_elem;
+  uint64_t ntiles;
+  uint64_t vec_bytes;
+  int32_t n_shares;
+  int32_t threshold;  // runtime t (generic kernel only)
+};
+
+constexpr int kBlock = 256;  // 4 waves
+constexpr int kWavesPerBlock = kBlock / 64;
+
+template <bool FE_SECRET>
+__device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, uint32_t w, uint32_t c0[kLimbs]) {
+  if constexpr (FE_SECRET) {
+    load_fe(tile_base(a.sec_fe, tile), w, c0);
+  } else {
+    const int64_t* sec = a.sec_u64 + static_cast<uint64_t>(tile) * kTile;  // uniform base
+    const uint64_t s = static_cast<uint64_t>(__builtin_nontemporal_load(sec + w));
+    c0[0] = static_cast<uint32_t>(s);
+    c0[1] = static_cast<uint32_t>(s >> 32);
+#pragma unroll
+    for (int i = 2; i < kLimbs; ++i) c0[i] = 0u;
+  }
+}
+
+// T = compile-time threshold (1..8).  FOLD: fold after every Horner step
+// (needed when sum_{j<T} n^j >= 2^23, i.e. the unreduced value could pass
+// 2^544); otherwise only the final value is reduced.
+template <int T, bool FE_SECRET, bool FOLD>
+__global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t w = lane + 64u * q;
+      const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
+      if (e >= a.n_elem) break;
+      uint32_t c[T][kLimbs];
+      load_secret<FE_SECRET>(a, tile, w, c[0]);
+#pragma unroll
+      for (int j = 1; j < T; ++j) load_fe(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.vec_bytes, tile), w, c[j]);
+#pragma unroll 1
+      for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+        const uint32_t x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(xi));
+        uint32_t v[kLimbs];
+        if constexpr (T == 1) {
+#pragma unroll
+          for (int i = 0; i < kLimbs; ++i) v[i] = c[0][i];
+        } else {
+          mul_small_add(v, c[T - 1], x, c[T - 2]);
+          if constexpr (FOLD && T > 2) fold(v);
+#pragma unroll
+          for (int j = T - 3; j >= 0; --j) {
+            mul_small_add(v, x, c[j]);
+            if constexpr (FOLD) {
+              if (j > 0) fold(v);
+            }
+          }
+        }
+        reduce(v);
+        store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, v);
+      }
+    }
+  }
+}
+
+// Generic threshold (any t <= 64): coefficients are re-read per share through
+// the caches instead of being held in registers; always folds.
+template <bool FE_SECRET>
+__global__ void __launch_bounds__(kBlock) split_kernel_generic(const SplitArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t w = lane + 64u * q;
+      const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
+      if (e >= a.n_elem) break;
+      uint32_t c0[kLimbs];
+      load_secret<FE_SECRET>(a, tile, w, c0);
+#pragma unroll 1
+      for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+        const uint32_t x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(xi));
+        uint32_t v[kLimbs];
+        load_fe_cached(tile_base(a.coeffs + static_cast<uint64_t>(a.threshold - 2) * a.vec_bytes, tile), w, v);
+#pragma unroll 1
+        for (int j = a.threshold - 3; j >= 0; --j) {
+          uint32_t cj[kLimbs];
+          load_fe_cached(tile_base(a.coeffs + static_cast<uint64_t>(j) * a.vec_bytes, tile), w, cj);
+          mul_small_add(v, x, cj);
+          fold(v);
+        }
+        mul_small_add(v, x, c0);
+        reduce(v);
+        store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, v);
+      }
+    }
+  }
+}
+
+struct ReconArgs {
+  const uint8_t* shares[DN_MAX_RESOLVE];
+  uint8_t* out_fe;
+  int64_t* out_u64;
+  uint32_t* overflow;
+  uint64_t n_elem;
+  uint64_t ntiles;
+  int32_t k;
+  uint32_t neg;
+  uint32_t shift;
+  int32_t pad;
+  uint32_t a[DN_MAX_RESOLVE][kLimbs];
+  uint32_t inv[kLimbs];
+};
+
+// A = limbs of |a_i| (1, 2 or 17).  S = sum_i |a_i| * (y_i or p - y_i) is
+// accumulated unreduced in A + 17 limbs (value < 2^(521 + 32A + 4) for k <= 16;
+// for A = 17, a_i < p so < 2^1046), reduced once, then scaled by d^{-1}
+// (HAS_INV) and 2^{-shift} (a 521-bit rotation).
+template <int A, bool HAS_INV>
+__global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) {
+  constexpr int N = A + kLimbs;
+  constexpr int VB = (A == kLimbs) ? 1046 : (521 + 32 * A + 4);
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t w = lane + 64u * q;
+      const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
+      const bool valid = e < a.n_elem;
+      bool over = false;
+      if (valid) {
+        uint32_t S[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) S[i] = 0u;
+#pragma unroll 1
+        for (int32_t i = 0; i < a.k; ++i) {
+          uint32_t y[kLimbs];
+          load_fe(tile_base(a.shares[i], tile), w, y);
+          if ((a.neg >> i) & 1u) {  // -y == p - y == ~y within 521 bits
+#pragma unroll
+            for (int l = 0; l < 16; ++l) y[l] = ~y[l];
+            y[16] = (~y[16]) & kTopMask;
+          }
+          mac_wide<N, A>(S, a.a[i], y);
+        }
+        uint32_t r[kLimbs];
+        reduce_wide<N, VB>(S, r);
+        if constexpr (HAS_INV) {
+          uint32_t t[kLimbs];
+          mulmod(t, r, a.inv);
+#pragma unroll
+          for (int l = 0; l < kLimbs; ++l) r[l] = t[l];
+        }
+        if (a.shift != 0u) rotr521(r, a.shift);
+        if (a.out_fe) store_fe(tile_base(a.out_fe, tile), w, r);
+        if (a.out_u64) {
+          const uint64_t lo = static_cast<uint64_t>(r[0]) | (static_cast<uint64_t>(r[1]) << 32);
+          __builtin_nontemporal_store(static_cast<int64_t>(lo), a.out_u64 + static_cast<uint64_t>(tile) * kTile + w);
+        }
+        uint32_t hi_or = 0u;
+#pragma unroll
+        for (int l = 2; l < kLimbs; ++l) hi_or |= r[l];
+        over = hi_or != 0u;
+      }
+      if (a.overflow) {
+        const uint64_t m = __ballot(over);
+        if (lane == 0 && m) atomicAdd(a.overflow, static_cast<uint32_t>(__popcll(m)));
+      }
+      if (!valid) break;
+    }
+  }
+}
+
+static int grid_for(uint64_t ntiles) {
+  static const int cap = [] {
+    const char* s = std::getenv("DN_GRID_CAP");
+    const int v = s ? std::atoi(s) : 0;
+    return v > 0 ? v : 4096;
+  }();
+  const uint64_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+  return static_cast<int>(blocks < static_cast<uint64_t>(cap) ? blocks : static_cast<uint64_t>(cap));
+}
+
+static int check_launch(const char* what) {
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: launch failed: %s", what, hipGetErrorString(err));
+  return DN_OK;
+}
+
+// sum_{j<t} n^j < 2^23  <=>  the unreduced Horner value stays below 2^544.
+static bool needs_fold(int t, int n) {
+  double s = 0.0, p = 1.0;
+  for (int j = 0; j < t; ++j) {
+    s += p;
+    p *= n;
+  }
+  return s >= 8388608.0;
+}
+
+template <bool FE_SECRET, bool FOLD>
+static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
+  switch (t) {
+    case 1: hipLaunchKernelGGL((split_kernel<1, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((split_kernel<2, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((split_kernel<4, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((split_kernel<5, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((split_kernel<6, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((split_kernel<7, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((split_kernel<8, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    default: hipLaunchKernelGGL((split_kernel_generic<FE_SECRET>), g, dim3(kBlock), 0, s, a); break;
+  }
+}
+
+static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, bool fe, const char* name) {
+  if (threshold < 1 || threshold > DN_MAX_THRESHOLD)
+    return set_error(DN_ERR_UNSUPPORTED, "%s: threshold %d outside 1..%d", name, threshold, DN_MAX_THRESHOLD);
+  if (threshold > n_shares) return set_error(DN_ERR_THRESHOLD, "threshold should be little equal than shares");
+  if (n_shares > DN_MAX_SHARES)
+    return set_error(DN_ERR_UNSUPPORTED, "%s: %d shares > %d", name, n_shares, DN_MAX_SHARES);
+  if (a.n_elem == 0) return DN_OK;
+  if (!a.shares || (threshold > 1 && !a.coeffs) || (fe ? !a.sec_fe : !a.sec_u64))
+    return set_error(DN_ERR_ARG, "%s: null pointer", name);
+  a.ntiles = (a.n_elem + kTile - 1) / kTile;
+  a.vec_bytes = a.ntiles * kTileBytes;
+  a.n_shares = n_shares;
+  a.threshold = threshold;
+  const dim3 g(grid_for(a.ntiles));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool fold_each = needs_fold(threshold, n_shares);
+  if (fe) {
+    if (fold_each) launch_split_t<true, true>(threshold, g, s, a);
+    else launch_split_t<true, false>(threshold, g, s, a);
+  } else {
+    if (fold_each) launch_split_t<false, true>(threshold, g, s, a);
+    else launch_split_t<false, false>(threshold, g, s, a);
+  }
+  return check_launch(name);
+}
+
+}  // namespace dn
+
+using namespace dn;
+
+extern "C" int dn_m521_split_u64(const int64_t* secrets, const void* coeffs, void* shares, uint64_t n_elem,
+                                 int threshold, int n_shares, void* stream) {
+  SplitArgs a{};
+  a.sec_u64 = secrets;
+  a.coeffs = static_cast<const uint8_t*>(coeffs);
+  a.shares = static_cast<uint8_t*>(shares);
+  a.n_elem = n_elem;
+  return split_common(a, threshold, n_shares, stream, false, "dn_m521_split_u64");
+}
+
+extern "C" int dn_m521_split_fe(const void* secrets_fe, const void* coeffs, void* shares, uint64_t n_elem,
+                                int threshold, int n_shares, void* stream) {
+  SplitArgs a{};
+  a.sec_fe = static_cast<const uint8_t*>(secrets_fe);
+  a.coeffs = static_cast<const uint8_t*>(coeffs);
+  a.shares = static_cast<uint8_t*>(shares);
+  a.n_elem = n_elem;
+  return split_common(a, threshold, n_shares, stream, true, "dn_m521_split_fe");
+}
+
+extern "C" int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_lagrange_t* w, void* out_fe,
+                                   int64_t* out_u64, uint32_t* overflow_count, uint64_t n_elem, void* stream) {
+  if (!w || !share_vecs) return set_error(DN_ERR_ARG, "dn_m521_reconstruct: null pointer");
+  if (w->k < 1 || w->k > DN_MAX_RESOLVE)
+    return set_error(DN_ERR_UNSUPPORTED, "dn_m521_reconstruct: k=%d outside 1..%d", w->k, DN_MAX_RESOLVE);
+  if (!(w->a_limbs == 1 || w->a_limbs == 2 || w->a_limbs == 17) || w->shift < 0 || w->shift > 31)
+    return set_error(DN_ERR_ARG, "dn_m521_reconstruct: malformed weights");
+  if (n_elem == 0) return DN_OK;
+  if (!out_fe && !out_u64) return set_error(DN_ERR_ARG, "dn_m521_reconstruct: no output");
+  ReconArgs a{};
+  for (int i = 0; i < w->k; ++i) {
+    if (!share_vecs[i]) return set_error(DN_ERR_ARG, "dn_m521_reconstruct: null share vector %d", i);
+    a.shares[i] = static_cast<const uint8_t*>(share_vecs[i]);
+  }
+  a.out_fe = static_cast<uint8_t*>(out_fe);
+  a.out_u64 = out_u64;
+  a.overflow = overflow_count;
+  a.n_elem = n_elem;
+  a.ntiles = (n_elem + kTile - 1) / kTile;
+  a.k = w->k;
+  a.neg = w->neg;
+  a.shift = static_cast<uint32_t>(w->shift);
+  std::memcpy(a.a, w->a, sizeof(a.a));
+  std::memcpy(a.inv, w->inv, sizeof(a.inv));
+  const dim3 g(grid_for(a.ntiles));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool inv = w->has_inv != 0;
+  switch (w->a_limbs) {
+    case 1:
+      if (inv) hipLaunchKernelGGL((reconstruct_kernel<1, true>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((reconstruct_kernel<1, false>), g, dim3(kBlock), 0, s, a);
+      break;
+    case 2:
+      if (inv) hipLaunchKernelGGL((reconstruct_kernel<2, true>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((reconstruct_kernel<2, false>), g, dim3(kBlock), 0, s, a);
+      break;
+    default:
+      if (inv) hipLaunchKernelGGL((reconstruct_kernel<17, true>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((reconstruct_kernel<17, false>), g, dim3(kBlock), 0, s, a);
+      break;
+  }
+  return check_launch("dn_m521_reconstruct");
+}

@@ -1,0 +1,215 @@
+"""ctypes binding of the C-ABI library `libdn_shamir.so` (include/dn_shamir.h).
+
+The product path is the HIP library: there is no CPU fallback.  If the
+library is missing, or no HIP device is visible when a device call is made,
+these helpers raise instead of computing anything on the host.
+
+torch is imported before the library is loaded so that the library's
+`libamdhip64.so.7` dependency resolves to the HIP runtime torch already
+loaded (same soname), i.e. one runtime, one set of streams per process.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+DN_OK = 0
+DN_ERR_ARG = -1
+DN_ERR_THRESHOLD = -2
+DN_ERR_TOO_FEW = -3
+DN_ERR_DISTINCT = -4
+DN_ERR_HIP = -5
+DN_ERR_UNSUPPORTED = -6
+DN_ERR_EMPTY = -7
+
+MAX_RESOLVE = 16
+MAX_THRESHOLD = 64
+MAX_SHARES = 65535
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_LIB = os.path.normpath(os.path.join(_HERE, "..", "..", "..", "lib", "libdn_shamir.so"))
+
+# Every symbol include/dn_shamir.h declares (checked by the CPU test suite).
+EXPORTS = (
+    "dn_m521_vec_bytes", "dn_m521_split_u64", "dn_m521_split_fe", "dn_m521_lagrange",
+    "dn_m521_reconstruct", "dn_mt19937_draw_coeffs", "dn_last_error", "dn_version",
+)
+
+
+class Lagrange(ctypes.Structure):
+    """Mirror of dn_m521_lagrange_t."""
+
+    _fields_ = [
+        ("k", ctypes.c_int32),
+        ("a_limbs", ctypes.c_int32),
+        ("neg", ctypes.c_uint32),
+        ("shift", ctypes.c_int32),
+        ("has_inv", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("a", (ctypes.c_uint32 * 17) * MAX_RESOLVE),
+        ("inv", ctypes.c_uint32 * 17),
+    ]
+
+
+_lock = threading.Lock()
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib_path() -> str:
+    return os.environ.get("DN_SHAMIR_LIB", DEFAULT_LIB)
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (bind the HIP runtime torch already loaded)
+
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"libdn_shamir.so not found at {path}: build it with `make -C delta-node_amd` "
+                "(or __graft_entry__.build()); the Shamir hot path has no CPU fallback")
+        L = ctypes.CDLL(path)
+        vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        L.dn_m521_vec_bytes.restype = u64
+        L.dn_m521_vec_bytes.argtypes = [u64]
+        L.dn_m521_split_u64.restype = i32
+        L.dn_m521_split_u64.argtypes = [vp, vp, vp, u64, i32, i32, vp]
+        L.dn_m521_split_fe.restype = i32
+        L.dn_m521_split_fe.argtypes = [vp, vp, vp, u64, i32, i32, vp]
+        L.dn_m521_lagrange.restype = i32
+        L.dn_m521_lagrange.argtypes = [ctypes.POINTER(ctypes.c_uint64), i32, i32, ctypes.POINTER(Lagrange)]
+        L.dn_m521_reconstruct.restype = i32
+        L.dn_m521_reconstruct.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(Lagrange), vp, vp, vp, u64, vp]
+        L.dn_mt19937_draw_coeffs.restype = i32
+        L.dn_mt19937_draw_coeffs.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64,
+                                             i32, vp]
+        L.dn_last_error.restype = ctypes.c_char_p
+        L.dn_last_error.argtypes = []
+        L.dn_version.restype = ctypes.c_char_p
+        L.dn_version.argtypes = []
+        _lib = L
+        return L
+
+
+def last_error() -> str:
+    return lib().dn_last_error().decode()
+
+
+def check(rc: int) -> None:
+    """Map a DN_ERR_* code to the reference's exception type (shamir.py:57,73,75)."""
+    if rc == DN_OK:
+        return
+    msg = last_error()
+    if rc in (DN_ERR_THRESHOLD, DN_ERR_TOO_FEW, DN_ERR_DISTINCT, DN_ERR_ARG):
+        raise ValueError(msg)
+    if rc == DN_ERR_EMPTY:
+        raise TypeError(msg)
+    if rc == DN_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(f"dn_shamir error {rc}: {msg}")
+
+
+# ------------------------------------------------------------------ device
+def require_device():
+    """The current HIP device; raise if there is none (no CPU fallback)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        raise RuntimeError("delta_node.crypto.shamir: no HIP device visible; the MI355X path has no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr() -> int:
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def vec_bytes(n: int) -> int:
+    return int(lib().dn_m521_vec_bytes(n))
+
+
+def split_u64(secrets, coeffs, shares, n: int, t: int, n_shares: int) -> None:
+    check(lib().dn_m521_split_u64(_ptr(secrets), _ptr(coeffs), _ptr(shares), n, t, n_shares, stream_ptr()))
+
+
+def split_fe(secrets_fe, coeffs, shares, n: int, t: int, n_shares: int) -> None:
+    check(lib().dn_m521_split_fe(_ptr(secrets_fe), _ptr(coeffs), _ptr(shares), n, t, n_shares, stream_ptr()))
+
+
+def lagrange(xs: Sequence[int], threshold: int) -> Lagrange:
+    w = Lagrange()
+    arr = (ctypes.c_uint64 * max(1, len(xs)))(*[int(x) for x in xs])
+    check(lib().dn_m521_lagrange(arr, len(xs), threshold, ctypes.byref(w)))
+    return w
+
+
+def generic_weights(lams: Sequence[int]) -> Lagrange:
+    """Descriptor for explicit weights lambda_i in [0, p) (full-width form)."""
+    if not 1 <= len(lams) <= MAX_RESOLVE:
+        raise ValueError("generic_weights: 1..16 weights")
+    w = Lagrange()
+    w.k = len(lams)
+    w.a_limbs = 17
+    for i, lam in enumerate(lams):
+        for j in range(17):
+            w.a[i][j] = (lam >> (32 * j)) & 0xFFFFFFFF
+    return w
+
+
+def ones_weights(k: int) -> Lagrange:
+    """Descriptor summing k vectors mod p (all lambda_i = 1)."""
+    w = Lagrange()
+    w.k = k
+    w.a_limbs = 1
+    for i in range(k):
+        w.a[i][0] = 1
+    return w
+
+
+def reconstruct(share_vecs: Sequence, w: Lagrange, out_fe=None, out_u64=None, overflow=None, n: int = 0) -> None:
+    k = len(share_vecs)
+    if k != w.k:
+        raise ValueError("reconstruct: weight/share count mismatch")
+    ptrs = (ctypes.c_void_p * k)(*[v.data_ptr() for v in share_vecs])
+    check(lib().dn_m521_reconstruct(ptrs, ctypes.byref(w), _ptr(out_fe), _ptr(out_u64), _ptr(overflow), n,
+                                    stream_ptr()))
+
+
+def mt_draw_coeffs(rng, n: int, tm1: int) -> np.ndarray:
+    """Draw n*(t-1) coefficients from `rng` (a random.Random) exactly as n
+    sequential `make_shares` calls would (shamir.py:59-61), into a host block
+    of tm1 tiled vectors; `rng`'s state advances identically."""
+    vb = vec_bytes(n)
+    out = np.zeros(max(tm1, 0) * vb, dtype=np.uint8)
+    if tm1 <= 0 or n == 0:
+        return out.reshape(max(tm1, 0), vb)
+    version, internal, gauss = rng.getstate()
+    state = (ctypes.c_uint32 * 624)(*internal[:624])
+    index = ctypes.c_int32(internal[624])
+    check(lib().dn_mt19937_draw_coeffs(state, ctypes.byref(index), n, tm1, out.ctypes.data))
+    rng.setstate((version, tuple(state) + (index.value,), gauss))
+    return out.reshape(tm1, vb)
+
+
+def version() -> str:
+    return lib().dn_version().decode()
+
+
+def exported_symbols() -> List[str]:
+    L = lib()
+    return [s for s in EXPORTS if hasattr(L, s)]

@@ -1,0 +1,283 @@
+"""Shamir secret sharing over GF(2^521 - 1) — the `delta_node.crypto.shamir` surface.
+
+Drop-in for delta_node/crypto/shamir/shamir.py (same names, arguments, return
+values and exceptions), backed by the MI355X HIP library through its C-ABI
+(`_native`, include/dn_shamir.h):
+
+=============================  =============================================
+reference (shamir.py)          here
+=============================  =============================================
+``Share``, ``PRIME`` :14-16    same objects
+``_eval_at`` :19-25            device Horner (`dn_m521_split_fe`)
+``_share_to_bytes`` :28-33     same codec (host, per share)
+``_bytes_to_share`` :36-45     same codec (host, per share)
+``SecretShare.__init__`` :49   same attributes: threshold, prime, random
+``make_shares`` :55-66         coefficients from ``self.random`` exactly as
+                               the reference draws them; evaluation on GPU
+``resolve_shares`` :68-90      same checks/messages; Lagrange weights on the
+                               host (once per call), interpolation on GPU
+=============================  =============================================
+
+Vector extension (the hot path, new): ``make_shares_vec`` splits a whole
+int64 tensor, element e behaving exactly like
+``make_shares(v_e.to_bytes(8, "big", signed=True), n)`` called in order on the
+same instance; ``resolve_shares_vec`` interpolates whole share vectors.
+
+There is no CPU fallback: without the native library or a HIP device every
+call raises.  Only the default prime (the Mersenne prime M521) is supported;
+``SecretShare(t, prime=q)`` with another q raises NotImplementedError.
+"""
+from __future__ import annotations
+
+import random
+from functools import reduce
+from typing import List, Optional, Sequence, Tuple, Union
+
+from ... import serialize
+from . import _native, field, op
+
+__all__ = ["Share", "PRIME", "SecretShare"]
+
+Share = Tuple[int, int]
+
+PRIME = (1 << 521) - 1  # 0x01FF...FF, the Mersenne prime M521 (shamir.py:16)
+
+
+# ------------------------------------------------------------------ codec
+def _share_to_bytes(share: Share) -> bytes:
+    """``[len(x) as 1 byte][x minimal BE][y minimal BE]`` (shamir.py:28-33)."""
+    x, y = share
+    xb = serialize.int_to_bytes(x)
+    return len(xb).to_bytes(1, "big") + xb + serialize.int_to_bytes(y)
+
+
+def _bytes_to_share(data: bytes) -> Share:
+    """Inverse of `_share_to_bytes` (shamir.py:36-45)."""
+    xl = int.from_bytes(data[:1], "big")
+    return serialize.bytes_to_int(data[1:1 + xl]), serialize.bytes_to_int(data[1 + xl:])
+
+
+# ------------------------------------------------------- device helpers
+def _device():
+    _native.lib()
+    return _native.require_device()
+
+
+def _to_device_vecs(ints: Sequence[int], dev):
+    """Python ints (each < 2^521) -> uint8 device tensor [len, vec_bytes(1)]."""
+    import numpy as np
+    import torch
+
+    host = np.stack([field.ints_to_vec([v]) for v in ints]) if ints else np.zeros((0, field.vec_bytes(1)), np.uint8)
+    return torch.from_numpy(host).to(dev)
+
+
+def _eval_many(coeffs: Sequence[int], n_shares: int) -> List[int]:
+    """y(x) = sum_j coeffs[j] x^j mod p for x = 1..n_shares, on the GPU.
+    coeffs[0] is the secret (any size; reduced mod p here)."""
+    import torch
+
+    dev = _device()
+    t = len(coeffs)
+    sec = _to_device_vecs([coeffs[0] % PRIME], dev)
+    cof = _to_device_vecs(list(coeffs[1:]), dev) if t > 1 else None
+    out = torch.empty((n_shares, field.vec_bytes(1)), dtype=torch.uint8, device=dev)
+    _native.split_fe(sec, cof, out, 1, t, n_shares)
+    host = out.cpu().numpy()
+    return [field.vec_to_ints(host[i], 1)[0] for i in range(n_shares)]
+
+
+def _eval_at(coeffs: List[int], x: int, prime: int) -> int:
+    """Horner evaluation of `coeffs` at x mod prime (shamir.py:19-25), on the GPU."""
+    if prime != PRIME:
+        raise NotImplementedError("the MI355X Shamir path supports only the default prime 2^521 - 1")
+    if not coeffs:
+        return 0
+    if x == 0:
+        return coeffs[0] % prime
+    if not 1 <= x <= _native.MAX_SHARES or len(coeffs) > _native.MAX_THRESHOLD:
+        raise NotImplementedError("_eval_at: x must be in 1..65535 and len(coeffs) <= 64")
+    return _eval_many([c % prime for c in coeffs], x)[x - 1]
+
+
+def _lagrange_generic(xs: Sequence[int], prime: int) -> List[int]:
+    """lambda_i = prod_{j!=i} (-x_j) / prod_{j!=i} (x_i - x_j) mod p, as the
+    reference forms nums/dens (shamir.py:77-83) and divides (op.py:28-29)."""
+    k = len(xs)
+    lams = []
+    for i in range(k):
+        num = reduce(lambda a, b: a * b, [-xs[j] for j in range(k) if j != i])
+        den = reduce(lambda a, b: a * b, [xs[i] - xs[j] for j in range(k) if j != i])
+        lams.append(op.div_mod(num % prime, den, prime))
+    return lams
+
+
+def _resolve_vectors(vecs: Sequence, xs: Sequence[int], n: int, threshold: int,
+                     out_fe=None, out_u64=None, overflow=None) -> None:
+    """Lagrange-at-0 of device share vectors `vecs` (abscissas xs) into
+    out_fe / out_u64, on the GPU.  k <= 16 with 64-bit xs uses the native
+    small-rational weights; otherwise full-width weights in groups of 16 whose
+    partial vectors are then summed mod p on the device."""
+    import torch
+
+    k = len(xs)
+    if k <= _native.MAX_RESOLVE and all(0 <= int(x) < (1 << 64) for x in xs):
+        w = _native.lagrange(xs, threshold)
+        _native.reconstruct(vecs, w, out_fe=out_fe, out_u64=out_u64, overflow=overflow, n=n)
+        return
+    lams = _lagrange_generic([int(x) for x in xs], PRIME)
+    vb = field.vec_bytes(n)
+    dev = vecs[0].device
+    G = _native.MAX_RESOLVE
+    parts = []
+    for g in range(0, k, G):
+        part = torch.empty(vb, dtype=torch.uint8, device=dev)
+        _native.reconstruct(vecs[g:g + G], _native.generic_weights(lams[g:g + G]), out_fe=part, n=n)
+        parts.append(part)
+    while len(parts) > G:  # sum partial vectors mod p, 16 at a time
+        merged = []
+        for g in range(0, len(parts), G):
+            dst = torch.empty(vb, dtype=torch.uint8, device=dev)
+            _native.reconstruct(parts[g:g + G], _native.ones_weights(len(parts[g:g + G])), out_fe=dst, n=n)
+            merged.append(dst)
+        parts = merged
+    _native.reconstruct(parts, _native.ones_weights(len(parts)), out_fe=out_fe, out_u64=out_u64,
+                        overflow=overflow, n=n)
+
+
+# ------------------------------------------------------------------ API
+class SecretShare(object):
+    """Threshold-`threshold` Shamir scheme over GF(PRIME) (shamir.py:48-90)."""
+
+    def __init__(self, threshold: int, *, prime: int = PRIME):
+        if prime != PRIME:
+            raise NotImplementedError("the MI355X Shamir path supports only the default prime 2^521 - 1")
+        self.threshold = threshold
+        self.prime = prime
+        self.random = random.Random()
+
+    # ---- reference byte API -------------------------------------------
+    def make_shares(self, value: bytes, shares: int) -> List[bytes]:
+        """Split `value` into `shares` byte shares (shamir.py:55-66)."""
+        if self.threshold > shares:
+            raise ValueError("threshold should be little equal than shares")
+        coeffs = [serialize.bytes_to_int(value)] + [
+            self.random.randint(1, self.prime - 1) for _ in range(self.threshold - 1)
+        ]
+        if shares <= 0:
+            return []
+        if shares > _native.MAX_SHARES or len(coeffs) > _native.MAX_THRESHOLD:
+            raise NotImplementedError("make_shares: at most 65535 shares and threshold 64 on the device path")
+        ys = _eval_many(coeffs, shares)
+        return [_share_to_bytes((x, y)) for x, y in zip(range(1, shares + 1), ys)]
+
+    def resolve_shares(self, shares: List[bytes]) -> bytes:
+        """Recover the secret from byte shares (shamir.py:68-90): the
+        Lagrange interpolant of ALL given shares at 0, minimal big-endian."""
+        import torch
+
+        share_tups = [_bytes_to_share(share) for share in shares]
+        xs, ys = zip(*share_tups)
+        k = len(xs)
+        if k < self.threshold:
+            raise ValueError("need at least {} shares".format(self.threshold))
+        if k != len(set(xs)):
+            raise ValueError("shares must be distinct")
+        if k == 1:  # the reference's reduce() over an empty product list
+            raise TypeError("reduce() of empty iterable with no initial value")
+        dev = _device()
+        vecs = list(_to_device_vecs([y % PRIME for y in ys], dev).unbind(0))
+        out = torch.empty(field.vec_bytes(1), dtype=torch.uint8, device=dev)
+        _resolve_vectors(vecs, xs, 1, self.threshold, out_fe=out)
+        return serialize.int_to_bytes(field.vec_to_ints(out.cpu().numpy(), 1)[0])
+
+    # ---- vector extension (the hot path) -------------------------------
+    def draw_coeffs_vec(self, n: int, device=None):
+        """The (t-1) x n coefficients that n sequential `make_shares` calls
+        would draw from `self.random` (advancing it identically), as a uint8
+        device tensor [t-1, vec_bytes(n)] in the tiled layout."""
+        import torch
+
+        dev = device if device is not None else _device()
+        host = _native.mt_draw_coeffs(self.random, n, max(self.threshold, 1) - 1)
+        return torch.from_numpy(host).to(dev)
+
+    def make_shares_vec(self, values, shares: int, *, coeffs=None, out=None):
+        """Split every element of an int64 tensor.
+
+        values  int64 tensor [N] (any device; copied to the current HIP device)
+        coeffs  optional uint8 device tensor [t-1, vec_bytes(N)]; default: drawn
+                from `self.random` as N sequential `make_shares` calls would
+        out     optional uint8 device tensor [shares, vec_bytes(N)]
+        Returns uint8 device tensor [shares, vec_bytes(N)]: row x-1 holds share x
+        of every element (tiled M521 layout, canonical residues).
+        """
+        import torch
+
+        if self.threshold > shares:
+            raise ValueError("threshold should be little equal than shares")
+        if shares > _native.MAX_SHARES or self.threshold > _native.MAX_THRESHOLD:
+            raise NotImplementedError("make_shares_vec: at most 65535 shares and threshold 64")
+        dev = _device()
+        vals = torch.as_tensor(values)
+        if vals.dtype not in (torch.int64, torch.uint64):
+            raise TypeError("make_shares_vec: values must be an int64 tensor")
+        vals = vals.reshape(-1).to(dev).contiguous()
+        n = vals.numel()
+        t = max(self.threshold, 1)
+        vb = field.vec_bytes(n)
+        if coeffs is None:
+            coeffs = self.draw_coeffs_vec(n, dev) if t > 1 else None
+        elif t > 1:
+            if coeffs.dtype != torch.uint8 or tuple(coeffs.shape) != (t - 1, vb) or coeffs.device != dev:
+                raise ValueError(f"make_shares_vec: coeffs must be uint8 [{t - 1}, {vb}] on {dev}")
+            coeffs = coeffs.contiguous()
+        if out is None:
+            out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
+        elif out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous():
+            raise ValueError(f"make_shares_vec: out must be contiguous uint8 [{shares}, {vb}]")
+        if shares > 0:
+            _native.split_u64(vals, coeffs if t > 1 else None, out, n, t, shares)
+        return out
+
+    def resolve_shares_vec(self, shares, xs: Sequence[int], n: int, *, out: str = "int64",
+                           return_overflow: bool = False):
+        """Interpolate share vectors at 0 (vector form of `resolve_shares`).
+
+        shares  sequence of k uint8 device tensors [vec_bytes(n)] (or a [k, vec_bytes(n)] tensor)
+        xs      their abscissas (share x of `make_shares_vec` is row x-1)
+        out     "int64": int64 tensor [n] holding the low 64 bits (the secret's
+                two's-complement view); "field": uint8 tiled vector [vec_bytes(n)]
+        return_overflow  also return a uint32 device counter of elements >= 2^64
+        Same checks as `resolve_shares` (too few, duplicates, k == 1).
+        """
+        import torch
+
+        vecs = list(shares.unbind(0)) if isinstance(shares, torch.Tensor) and shares.dim() == 2 else list(shares)
+        xs = [int(x) for x in xs]
+        if len(vecs) != len(xs):
+            raise ValueError("resolve_shares_vec: one abscissa per share vector")
+        if len(xs) == 0:
+            raise ValueError("not enough values to unpack (expected 2, got 0)")
+        k = len(xs)
+        if k < self.threshold:
+            raise ValueError("need at least {} shares".format(self.threshold))
+        if k != len(set(xs)):
+            raise ValueError("shares must be distinct")
+        if k == 1:
+            raise TypeError("reduce() of empty iterable with no initial value")
+        dev = _device()
+        vb = field.vec_bytes(n)
+        for v in vecs:
+            if v.dtype != torch.uint8 or v.numel() != vb or v.device != dev or not v.is_contiguous():
+                raise ValueError(f"resolve_shares_vec: share vectors must be contiguous uint8 [{vb}] on {dev}")
+        over = torch.zeros(1, dtype=torch.int32, device=dev) if return_overflow else None
+        if out == "int64":
+            res = torch.empty(n, dtype=torch.int64, device=dev)
+            _resolve_vectors(vecs, xs, n, self.threshold, out_u64=res, overflow=over)
+        elif out == "field":
+            res = torch.empty(vb, dtype=torch.uint8, device=dev)
+            _resolve_vectors(vecs, xs, n, self.threshold, out_fe=res, overflow=over)
+        else:
+            raise ValueError('resolve_shares_vec: out must be "int64" or "field"')
+        return (res, over) if return_overflow else res

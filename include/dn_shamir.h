@@ -1,0 +1,149 @@
+/*
+ * dn_shamir.h — C-ABI of the MI355X Shamir secret-sharing hot path
+ * (split = polynomial evaluation at x = 1..n, reconstruct = Lagrange
+ * interpolation at 0) over the Mersenne field GF(p), p = 2^521 - 1.
+ *
+ * Reference interface replaced (delta-mpc/delta-node, pure Python):
+ *   PRIME                            delta_node/crypto/shamir/shamir.py:16
+ *   _eval_at(coeffs, x, prime)       delta_node/crypto/shamir/shamir.py:19-25
+ *   SecretShare.make_shares          delta_node/crypto/shamir/shamir.py:55-66
+ *   SecretShare.resolve_shares       delta_node/crypto/shamir/shamir.py:68-90
+ *   op.extend_gcd/inverse_mod/div_mod delta_node/crypto/shamir/op.py:4-29
+ *   random.Random.randint (MT19937)  stdlib, drawn at shamir.py:59-61
+ * The reference has no FFI of its own; its boundary is the Python module
+ * `delta_node.crypto.shamir`, which this library backs (see INTEGRATION.md
+ * for the ctypes binding).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Device pointers are HIP device memory
+ *     owned by the caller; the library allocates nothing per call.
+ *   - Device entry points are asynchronous on `stream` (a hipStream_t, passed
+ *     as void*; NULL = the legacy default stream) and never synchronise.
+ *   - Return 0 (DN_OK) or a negative DN_ERR_* code; dn_last_error() returns a
+ *     thread-local message for the last failure on the calling thread.
+ *   - Re-entrant: no global mutable state besides that thread-local message.
+ *
+ * Field-element vector layout ("M521 tiled vector")
+ *   A vector of n field elements is cut into tiles of DN_M521_TILE (256)
+ *   elements; the last tile is padded.  Each tile is 16896 bytes:
+ *       uint32_t lo[16][256];   limb i (bits 32i..32i+31) of element w at lo[i][w]
+ *       uint16_t hi[256];       bits 512..520 of element w (bits 9..15 zero)
+ *   i.e. exactly 66 bytes per element (ceil(521/8)), struct-of-arrays inside
+ *   a tile so every wave access is a contiguous, coalesced run.  A vector
+ *   occupies dn_m521_vec_bytes(n) bytes; a "block" of S vectors is S such
+ *   vectors back to back (vector s at byte offset s * dn_m521_vec_bytes(n)).
+ *   Values are canonical residues in [0, p) on output; inputs must be < 2^521.
+ */
+#ifndef DN_SHAMIR_H
+#define DN_SHAMIR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DN_M521_LIMBS 17
+#define DN_M521_TILE 256
+#define DN_M521_TILE_BYTES 16896
+#define DN_MAX_THRESHOLD 64
+#define DN_MAX_SHARES 65535
+#define DN_MAX_RESOLVE 16
+
+enum {
+  DN_OK = 0,
+  DN_ERR_ARG = -1,         /* bad pointer / size / parameter                      */
+  DN_ERR_THRESHOLD = -2,   /* shamir.py:56-57  "threshold should be little equal than shares" */
+  DN_ERR_TOO_FEW = -3,     /* shamir.py:72-73  "need at least {t} shares"          */
+  DN_ERR_DISTINCT = -4,    /* shamir.py:74-75  "shares must be distinct"           */
+  DN_ERR_HIP = -5,         /* HIP runtime error (launch failure)                   */
+  DN_ERR_UNSUPPORTED = -6, /* outside the limits above                             */
+  DN_ERR_EMPTY = -7        /* shamir.py:78-83  k == 1: reduce() of empty iterable  */
+};
+
+/* Bytes of one tiled field-element vector of n elements (66 * round_up(n, 256)). */
+uint64_t dn_m521_vec_bytes(uint64_t n_elem);
+
+/*
+ * Split, int64 secrets (the vector path).  Element e behaves exactly like the
+ * reference `SecretShare(t).make_shares(v_e.to_bytes(8, "big", signed=True), n)`
+ * given that call's coefficients: share x (1..n) of element e is
+ *     y = (u64(v_e) + c_1 x + ... + c_{t-1} x^{t-1}) mod p
+ * (Horner as in `_eval_at`, shamir.py:19-25).
+ *   secrets  device int64[n_elem] (two's complement view = the reference's
+ *            big-endian 8-byte secret)
+ *   coeffs   device block of t-1 tiled vectors: vector j-1 holds c_j, each
+ *            in [1, p-1] as drawn at shamir.py:59-61 (may be NULL iff t == 1)
+ *   shares   device block of n_shares tiled vectors: vector x-1 = share x
+ * Replaces shamir.py:55-66 (+ _eval_at :19-25).  1 <= t <= 64, t <= n <= 65535.
+ */
+int dn_m521_split_u64(const int64_t* secrets, const void* coeffs, void* shares,
+                      uint64_t n_elem, int threshold, int n_shares, void* stream);
+
+/* Split with full field-element secrets (the byte API: c0 = bytes_to_int(value)
+ * mod p, a tiled vector).  Same contract as dn_m521_split_u64 otherwise. */
+int dn_m521_split_fe(const void* secrets_fe, const void* coeffs, void* shares,
+                     uint64_t n_elem, int threshold, int n_shares, void* stream);
+
+/*
+ * Lagrange-at-0 weights for share abscissas xs[0..k-1], in the form the
+ * reconstruct kernel consumes:  lambda_i = a_i / (d * 2^shift)  (mod p), with
+ * |a_i| held in a_limbs little-endian u32 limbs, sign bit i of `neg`, and
+ * inv = d^{-1} mod p when has_inv.  When the exact rationals do not fit, the
+ * generic form is used: a_i = lambda_i mod p (a_limbs = 17), has_inv = 0.
+ */
+typedef struct dn_m521_lagrange {
+  int32_t k;                             /* number of shares, 1..16           */
+  int32_t a_limbs;                       /* 1, 2 or 17                        */
+  uint32_t neg;                          /* bit i set: a_i is negative        */
+  int32_t shift;                         /* 0..31: final division by 2^shift  */
+  int32_t has_inv;                       /* multiply by inv                   */
+  int32_t reserved;
+  uint32_t a[DN_MAX_RESOLVE][DN_M521_LIMBS];
+  uint32_t inv[DN_M521_LIMBS];
+} dn_m521_lagrange_t;
+
+/* Host.  Validates like shamir.py:70-75 (k < threshold -> DN_ERR_TOO_FEW,
+ * duplicate x -> DN_ERR_DISTINCT, k == 1 -> DN_ERR_EMPTY) and fills *out.
+ * Replaces the weight computation of shamir.py:77-89 and op.py:4-29. */
+int dn_m521_lagrange(const uint64_t* xs, int k, int threshold, dn_m521_lagrange_t* out);
+
+/*
+ * Reconstruct: out_e = sum_i lambda_i * y_{i,e} mod p, canonical — the value
+ * `resolve_shares` returns (shamir.py:90) as an integer; ALL k shares are used
+ * (shamir.py:76-89), so inconsistent shares give the degree-(k-1) interpolant.
+ *   share_vecs    host array of k device pointers, each a tiled vector
+ *   out_fe        device tiled vector, or NULL
+ *   out_u64       device int64[n_elem] (low 64 bits of the result), or NULL
+ *   overflow_count device uint32 counter, incremented (atomically) once per
+ *                 element whose result is >= 2^64; may be NULL
+ * Replaces shamir.py:68-90.
+ */
+int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_lagrange_t* w,
+                        void* out_fe, int64_t* out_u64, uint32_t* overflow_count,
+                        uint64_t n_elem, void* stream);
+
+/*
+ * Host.  Draw the reference's coefficients with CPython's MT19937 semantics:
+ * for each element e (in order) and j = 1..t-1, c = randint(1, p-1) =
+ * 1 + getrandbits(521) rejected while >= p-1 (17 MT words, little-endian, last
+ * word >> 23) — exactly the calls shamir.py:59-61 makes on `self.random`.
+ *   mt_state  624 MT words (random.getstate()[1][:624]), updated in place
+ *   mt_index  the position (getstate()[1][624]), updated in place
+ *   coeffs    HOST block of t-1 tiled vectors (t-1 == tm1), written
+ */
+int dn_mt19937_draw_coeffs(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem,
+                           int tm1, void* coeffs);
+
+/* Thread-local message of the last failure (never NULL). */
+const char* dn_last_error(void);
+
+/* Library version string. */
+const char* dn_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DN_SHAMIR_H */

@@ -1,0 +1,60 @@
+"""ctypes wrapper of liboracle_m521.so (the C restatement).  Test infrastructure only."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "liboracle_m521.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run `make -C oracle` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB)
+        vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        L.oracle_draw_coeffs.argtypes = [u64, u64, i32, vp]
+        L.oracle_mt_words.argtypes = [u64, u64, vp]
+        L.oracle_split.argtypes = [vp, vp, u64, i32, i32, vp]
+        L.oracle_reconstruct.argtypes = [vp, vp, i32, u64, vp]
+        for f in (L.oracle_draw_coeffs, L.oracle_mt_words, L.oracle_split, L.oracle_reconstruct):
+            f.restype = None
+        _lib = L
+    return _lib
+
+
+def draw_coeffs(seed: int, n: int, tm1: int) -> np.ndarray:
+    """Coefficients random.Random(seed) yields for n make_shares calls: uint32 [n, tm1, 17]."""
+    out = np.zeros((n, tm1, 17), dtype=np.uint32)
+    if n and tm1:
+        lib().oracle_draw_coeffs(seed, n, tm1, out.ctypes.data)
+    return out
+
+
+def mt_words(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, dtype=np.uint32)
+    lib().oracle_mt_words(seed, n, out.ctypes.data)
+    return out
+
+
+def split(secrets: np.ndarray, coeffs: np.ndarray, t: int, n_shares: int) -> np.ndarray:
+    """secrets int64 [n], coeffs uint32 [n, t-1, 17] -> shares uint32 [n_shares, n, 17]."""
+    sec = np.ascontiguousarray(secrets).view(np.uint64)
+    n = sec.shape[0]
+    cof = np.ascontiguousarray(coeffs, dtype=np.uint32)
+    out = np.zeros((n_shares, n, 17), dtype=np.uint32)
+    lib().oracle_split(sec.ctypes.data, cof.ctypes.data if cof.size else None, n, t, n_shares, out.ctypes.data)
+    return out
+
+
+def reconstruct(ys: np.ndarray, xs) -> np.ndarray:
+    """ys uint32 [k, n, 17], xs k small ints -> uint32 [n, 17]."""
+    ys = np.ascontiguousarray(ys, dtype=np.uint32)
+    k, n = ys.shape[0], ys.shape[1]
+    xa = np.array(xs, dtype=np.int64)
+    out = np.zeros((n, 17), dtype=np.uint32)
+    lib().oracle_reconstruct(ys.ctypes.data, xa.ctypes.data, k, n, out.ctypes.data)
+    return out

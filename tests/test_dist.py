@@ -1,0 +1,82 @@
+"""Multi-process element sharding (CPU, gloo, world_size 2 and 3).
+
+Each rank computes the shares of its tile-aligned shard (here with the C
+oracle standing in for the per-rank kernel — the device kernels are covered by
+the gpu tests), packs them into its padded block and all-gathers; the
+gathered vectors must equal the unsharded split byte for byte.  This is the
+data path `bench.py --allgather` and BASELINE config 4 use over RCCL.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from delta_node.crypto.shamir import dist as sdist
+from delta_node.crypto.shamir import field
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, N, t, n, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "delta-node_amd"), root, os.path.join(root, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import c_oracle
+    from golden.fixtures import secrets_int64
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sec = secrets_int64(3, N)
+        co = c_oracle.draw_coeffs(3, N, t - 1)
+        lo, hi = sdist.shard_range(N, rank, world)
+        B = sdist.shard_tiles(N, world) * field.TILE_BYTES
+        block = np.zeros((n, B), dtype=np.uint8)
+        if hi > lo:
+            sh = c_oracle.split(sec[lo:hi], co[lo:hi], t, n)  # [n, hi-lo, 17]
+            for x in range(n):
+                v = field.limbs_to_vec(sh[x])
+                block[x, : v.size] = v
+        full = sdist.allgather_share_blocks(torch.from_numpy(block), N)
+        if rank == 0:
+            want = c_oracle.split(sec, co, t, n)
+            ok = all(np.array_equal(full[x, : field.vec_bytes(N)].numpy(), field.limbs_to_vec(want[x]))
+                     for x in range(n))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N", [(2, 1000), (2, 512), (3, 1001)])
+def test_sharded_split_allgather_equals_unsharded(world, N):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, N, 3, 5, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=10) is True
+
+
+def test_shard_ranges_cover_exactly():
+    for N in (0, 1, 255, 256, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            ranges = [sdist.shard_range(N, r, world) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == N
+            for (a, b), (c, d) in zip(ranges, ranges[1:]):
+                assert b == c and (a % field.TILE == 0 or a == N)
+            assert all(hi - lo <= sdist.shard_tiles(N, world) * field.TILE for lo, hi in ranges)

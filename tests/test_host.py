@@ -1,0 +1,203 @@
+"""Host-side logic and the C-ABI boundary, on CPU (no kernel launches).
+
+* the library loads and exports every symbol include/dn_shamir.h declares;
+* the native MT19937 coefficient stream equals the reference's draws;
+* the Lagrange descriptors equal the reference's weights (as field values);
+* the tiled layout round-trips; the byte codec matches the reference's shares;
+* the reference's argument errors fire before any device work, and a device
+  call without a HIP device raises (no CPU fallback).
+"""
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from delta_node import serialize
+from delta_node.crypto import shamir
+from delta_node.crypto.shamir import _native, field, op
+from delta_node.crypto.shamir import shamir as shamir_mod
+from golden.fixtures import P, load_json, load_npz, manifest
+from oracle.py_shamir import RefSecretShare
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dn_shamir.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w ]+?\*?\s*\b(dn_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_header_symbols():
+    syms = header_symbols()
+    assert len(syms) >= 8
+    L = _native.lib()
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert sorted(_native.EXPORTS) == syms
+
+
+def test_version_and_sizes():
+    assert "gfx950" in _native.version()
+    for n in (0, 1, 255, 256, 257, 1 << 20, (1 << 24) + 3):
+        assert _native.vec_bytes(n) == field.vec_bytes(n) == 66 * 256 * ((n + 255) // 256)
+
+
+def test_field_layout_roundtrip():
+    rng = random.Random(3)
+    vals = [rng.randrange(P) for _ in range(700)] + [0, 1, P - 1]
+    vec = field.ints_to_vec(vals)
+    assert vec.size == field.vec_bytes(len(vals))
+    assert field.vec_to_ints(vec, len(vals)) == vals
+    planes = field.vec_to_planes(vec, len(vals))
+    assert field.limbs_to_ints(planes.T.copy()) == vals
+    # tile structure: element 300 is element 44 of tile 1, limb 3 at lo[3][44]
+    t = vec[field.TILE_BYTES:2 * field.TILE_BYTES]
+    lo = t[:64 * 256].view("<u4").reshape(16, 256)
+    assert lo[3, 44] == (vals[300] >> 96) & 0xFFFFFFFF
+    assert t[64 * 256:].view("<u2")[44] == vals[300] >> 512
+
+
+@pytest.mark.parametrize("key", ["f1", "f2"])
+def test_native_mt_coefficients_match_reference(key):
+    cfg = manifest()[key]
+    z = load_npz(cfg["file"])
+    r = random.Random(cfg["mt_seed"])
+    block = _native.mt_draw_coeffs(r, cfg["N"], cfg["t"] - 1)
+    got = np.stack([field.vec_to_limbs(block[j], cfg["N"]) for j in range(cfg["t"] - 1)], axis=1)
+    assert np.array_equal(got, z["coeff_limbs"])
+    # the Random object advanced exactly as the reference's calls advanced it
+    r2 = random.Random(cfg["mt_seed"])
+    for _ in range(cfg["N"] * (cfg["t"] - 1)):
+        r2.randint(1, P - 1)
+    assert r.getstate() == r2.getstate()
+    assert r.getrandbits(64) == r2.getrandbits(64)
+
+
+def test_native_mt_mid_stream_and_rejection_free_path():
+    r = random.Random(77)
+    r.getrandbits(32 * 100)  # start mid-buffer (index != 624)
+    r.random()
+    ref = random.Random()
+    ref.setstate(r.getstate())
+    block = _native.mt_draw_coeffs(r, 300, 2)
+    want = [ref.randint(1, P - 1) for _ in range(600)]
+    got = [field.vec_to_ints(block[j], 300) for j in range(2)]
+    assert [got[j][e] for e in range(300) for j in range(2)] == want
+    assert r.getstate() == ref.getstate()
+
+
+def _lam_ref(xs):
+    k = len(xs)
+    out = []
+    for i in range(k):
+        num, den = 1, 1
+        for j in range(k):
+            if j != i:
+                num *= -xs[j]
+                den *= xs[i] - xs[j]
+        out.append(op.div_mod(num % P, den, P))
+    return out
+
+
+def _lam_from_desc(w):
+    lams = []
+    k = w.k
+    scale = 1
+    if w.has_inv:
+        scale = sum(w.inv[j] << (32 * j) for j in range(17))
+    scale = scale * op.inverse_mod(pow(2, w.shift, P), P) % P
+    for i in range(k):
+        a = sum(w.a[i][j] << (32 * j) for j in range(w.a_limbs))
+        if (w.neg >> i) & 1:
+            a = -a
+        lams.append(a * scale % P)
+    return lams
+
+
+@pytest.mark.parametrize("xs", [
+    [1, 2, 3], [1, 3, 5], [2, 4, 5], [3, 4, 5], [5, 1, 3], [1, 2, 4, 5], [1, 2, 3, 4, 5], [1, 3, 5, 7, 9],
+    [2, 3, 5, 8, 9], [7, 100, 255], [1, 256, 1000], [2, 3], list(range(1, 10)), list(range(1, 17)),
+    [17, 33, 65, 129, 200, 250], [0, 5, 9], [1, 2**40, 2**63 + 7], [65535, 1, 300, 4096],
+    list(range(100, 116)), [2**64 - 1, 2**64 - 2, 3],
+])
+def test_lagrange_descriptor_equals_reference_weights(xs):
+    w = _native.lagrange(xs, 0)
+    assert w.k == len(xs) and w.a_limbs in (1, 2, 17) and 0 <= w.shift < 32
+    assert _lam_from_desc(w) == _lam_ref(xs)
+
+
+def test_lagrange_fast_forms():
+    w = _native.lagrange([1, 2, 3], 3)  # 3, -3, 1
+    assert (w.a_limbs, w.has_inv, w.shift, w.neg) == (1, 0, 0, 0b010)
+    w = _native.lagrange([1, 3, 5], 3)  # (15, -10, 3) / 8
+    assert (w.a_limbs, w.has_inv, w.shift) == (1, 0, 3)
+    w = _native.lagrange([2, 4, 5], 3)  # (10, -15, 8) / 3
+    assert (w.a_limbs, w.has_inv, w.shift) == (1, 1, 0)
+
+
+def test_lagrange_errors_mirror_reference():
+    with pytest.raises(ValueError, match="need at least 3 shares"):
+        _native.lagrange([1, 2], 3)
+    with pytest.raises(ValueError, match="shares must be distinct"):
+        _native.lagrange([1, 2, 1], 2)
+    with pytest.raises(TypeError, match="reduce"):
+        _native.lagrange([4], 1)
+    with pytest.raises(NotImplementedError):
+        _native.lagrange(list(range(1, 18)), 2)
+
+
+def test_share_codec_matches_reference_bytes():
+    f3 = load_json("f3_edge.json")
+    for case in f3["cases"][:40]:
+        for x, hx in enumerate(case["shares"], start=1):
+            b = bytes.fromhex(hx)
+            xx, y = shamir_mod._bytes_to_share(b)
+            assert xx == x
+            assert shamir_mod._share_to_bytes((xx, y)) == b
+
+
+def test_serialize_and_op_mirror():
+    for v in (0, 1, 255, 256, P, 2**64 - 1):
+        assert serialize.int_to_bytes(v) == v.to_bytes((v.bit_length() + 7) // 8, "big")
+        assert serialize.bytes_to_int(serialize.int_to_bytes(v)) == v
+    assert serialize.bytes_to_hex(b"\x01\x02", length=4) == "0x00000102"
+    assert serialize.hex_to_bytes("0x0102", length=3) == b"\x00\x01\x02"
+    assert op.inverse_mod(3, P) * 3 % P == 1
+    assert op.inverse_mod(-1, P) == P - 1
+    with pytest.raises(ZeroDivisionError):
+        op.inverse_mod(0, P)
+    assert op.div_mod(10, 5, P) == 2
+
+
+def test_surface_and_errors_before_device():
+    assert shamir_mod.__all__ == ["Share", "PRIME", "SecretShare"]
+    assert shamir.Share is shamir_mod.Share and shamir.SecretShare is shamir_mod.SecretShare
+    assert shamir.PRIME == P
+    ss = shamir.SecretShare(4)
+    assert ss.threshold == 4 and ss.prime == P and isinstance(ss.random, random.Random)
+    with pytest.raises(ValueError, match="threshold should be little equal than shares"):
+        ss.make_shares(b"\x01", 3)
+    sh = RefSecretShare(4).make_shares(b"\x05", 6)
+    with pytest.raises(ValueError, match="need at least 4 shares"):
+        ss.resolve_shares(sh[:3])
+    with pytest.raises(ValueError, match="shares must be distinct"):
+        ss.resolve_shares([sh[0], sh[1], sh[2], sh[1]])
+    with pytest.raises(ValueError, match="not enough values to unpack"):
+        ss.resolve_shares([])
+    with pytest.raises(TypeError):
+        shamir.SecretShare(1).resolve_shares(sh[:1])
+    with pytest.raises(NotImplementedError):
+        shamir.SecretShare(3, prime=2**127 - 1)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device failure mode")
+def test_no_cpu_fallback():
+    ss = shamir.SecretShare(2)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ss.make_shares(b"\x07", 3)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ss.make_shares_vec(torch.arange(10, dtype=torch.int64), 3)
