@@ -208,14 +208,15 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
   }
 }
 
+// Workgroups per launch: each 4-wave workgroup strides over tiles; 4096
+// workgroups = 16 per CU, enough waves to keep every CU's loads in flight.
+// DN_GRID_CAP overrides it (read per call; used by scripts/tune_kernels.py).
 static int grid_for(uint64_t ntiles) {
-  static const int cap = [] {
-    const char* s = std::getenv("DN_GRID_CAP");
-    const int v = s ? std::atoi(s) : 0;
-    return v > 0 ? v : 4096;
-  }();
+  const char* s = std::getenv("DN_GRID_CAP");
+  const int v = s ? std::atoi(s) : 0;
+  const uint64_t cap = v > 0 ? static_cast<uint64_t>(v) : 4096u;
   const uint64_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  return static_cast<int>(blocks < static_cast<uint64_t>(cap) ? blocks : static_cast<uint64_t>(cap));
+  return static_cast<int>(blocks < cap ? blocks : cap);
 }
 
 static int check_launch(const char* what) {
