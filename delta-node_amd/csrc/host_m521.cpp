@@ -14,6 +14,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -180,6 +181,25 @@ u128 gcd128(u128 a, u128 b) {
   return a;
 }
 
+// a^{-1} mod m for gcd(a, m) == 1, small m (extended Euclid).
+uint64_t inv_small(uint64_t a, uint64_t m) {
+  int64_t r0 = static_cast<int64_t>(m), r1 = static_cast<int64_t>(a % m), s0 = 0, s1 = 1;
+  while (r1) {
+    const int64_t q = r0 / r1, r2 = r0 - q * r1, s2 = s0 - q * s1;
+    r0 = r1;
+    r1 = r2;
+    s0 = s1;
+    s1 = s2;
+  }
+  return static_cast<uint64_t>((s0 % static_cast<int64_t>(m) + static_cast<int64_t>(m)) % static_cast<int64_t>(m));
+}
+
+// DN_EXACT_DIV=0 forces the full-width inverse (A/B and test hook).
+bool exact_div_disabled() {
+  const char* s = std::getenv("DN_EXACT_DIV");
+  return s && s[0] == '0';
+}
+
 bool mul_ovf(u128 a, u128 b, u128* out, u128 limit) {
   if (a == 0 || b == 0) {
     *out = 0;
@@ -307,9 +327,29 @@ extern "C" int dn_m521_lagrange(const uint64_t* xs, int k, int threshold, dn_m52
       out->shift = e;
     }
     if (d != 1) {
-      out->has_inv = 1;
-      const Fe inv = fe_pow_pm2(fe_u128(d));
-      std::memcpy(out->inv, inv.l, sizeof(out->inv));
+      out->d = static_cast<uint32_t>(d);
+      if (d < 65536u && (d & 1) && !exact_div_disabled()) {
+        // exact division by the small odd d (see dn_shamir.h)
+        const uint32_t d32 = static_cast<uint32_t>(d);
+        uint32_t inv32 = d32;  // Newton: x <- x (2 - d x), 5 steps from 3 correct bits
+        for (int it = 0; it < 5; ++it) inv32 *= 2u - d32 * inv32;
+        uint64_t pw = 1;  // 2^521 mod d, then p mod d = 2^521 - 1
+        for (int b = 0; b < 521; ++b) pw = (pw * 2) % d32;
+        const uint64_t pmod = (pw + d32 - 1) % d32;
+        out->has_inv = 2;
+        out->d_inv32 = inv32;
+        out->p_inv_d = static_cast<uint32_t>(inv_small(pmod, d32));
+        out->d_recip = UINT64_MAX / d32;
+        uint64_t wv = 1;
+        for (int i = 0; i < 17; ++i) {
+          out->w[i] = static_cast<uint32_t>(wv);
+          wv = (wv << 32) % d32;
+        }
+      } else {
+        out->has_inv = 1;
+        const Fe inv = fe_pow_pm2(fe_u128(d));
+        std::memcpy(out->inv, inv.l, sizeof(out->inv));
+      }
     }
     return DN_OK;
   }

@@ -203,4 +203,42 @@ __device__ __forceinline__ void rotr521(uint32_t v[kLimbs], uint32_t e) {
   }
 }
 
+// x mod d for x < 2^64 and d < 2^32, with recip = floor((2^64-1)/d)
+// (Barrett: the quotient estimate is low by at most one).
+__device__ __forceinline__ uint32_t mod_small(uint64_t x, uint32_t d, uint64_t recip) {
+  const uint64_t q = __umul64hi(x, recip);
+  uint64_t r = x - q * d;
+  if (r >= d) r -= d;
+  return static_cast<uint32_t>(r);
+}
+
+// r / d mod p for canonical r and a small odd d (3 <= d < 2^16).
+//   m = -r * p^{-1} mod d makes u = r + m*p divisible by d, and
+//   u / d <= (d p - 1) / d < p, so the quotient is already canonical.
+// u = r - m + m*2^521; the division runs LSB first (exact division, as in
+// GMP's divexact_1): q_i = (u_i - borrow) * d^{-1} mod 2^32, borrow = hi(q_i d).
+__device__ __forceinline__ void exact_div_small(uint32_t r[kLimbs], uint32_t d, uint32_t d_inv32, uint32_t p_inv_d,
+                                                uint64_t recip, const uint32_t* w) {
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) acc += static_cast<uint64_t>(r[i]) * w[i];  // < 17 * 2^48
+  const uint32_t rm = mod_small(acc, d, recip);
+  const uint32_t neg_r = rm ? d - rm : 0u;
+  const uint32_t m = mod_small(static_cast<uint64_t>(neg_r) * p_inv_d, d, recip);
+  r[16] += m << 9;  // + m * 2^521
+  unsigned b;
+  r[0] = __builtin_subc(r[0], m, 0u, &b);  // - m
+#pragma unroll
+  for (int i = 1; i < kLimbs; ++i) r[i] = __builtin_subc(r[i], 0u, b, &b);
+  uint32_t c = 0u;
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) {
+    const uint32_t s = r[i];
+    const uint32_t x = s - c;
+    const uint32_t q = x * d_inv32;
+    c = __umulhi(q, d) + (x > s ? 1u : 0u);
+    r[i] = q;
+  }
+}
+
 }  // namespace dn

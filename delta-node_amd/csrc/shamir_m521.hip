@@ -145,13 +145,17 @@ struct ReconArgs {
   int32_t pad;
   uint32_t a[DN_MAX_RESOLVE][kLimbs];
   uint32_t inv[kLimbs];
+  uint32_t d, d_inv32, p_inv_d, pad2;
+  uint64_t d_recip;
+  uint32_t w[kLimbs];
 };
 
 // A = limbs of |a_i| (1, 2 or 17).  S = sum_i |a_i| * (y_i or p - y_i) is
 // accumulated unreduced in A + 17 limbs (value < 2^(521 + 32A + 4) for k <= 16;
-// for A = 17, a_i < p so < 2^1046), reduced once, then scaled by d^{-1}
-// (HAS_INV) and 2^{-shift} (a 521-bit rotation).
-template <int A, bool HAS_INV>
+// for A = 17, a_i < p so < 2^1046), reduced once, then divided by d
+// (INV = 1: times d^{-1} mod p, a full product; INV = 2: exact division by a
+// small odd d) and by 2^shift (a 521-bit rotation).
+template <int A, int INV>
 __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) {
   constexpr int N = A + kLimbs;
   constexpr int VB = (A == kLimbs) ? 1046 : (521 + 32 * A + 4);
@@ -182,11 +186,13 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
         }
         uint32_t r[kLimbs];
         reduce_wide<N, VB>(S, r);
-        if constexpr (HAS_INV) {
+        if constexpr (INV == 1) {
           uint32_t t[kLimbs];
           mulmod(t, r, a.inv);
 #pragma unroll
           for (int l = 0; l < kLimbs; ++l) r[l] = t[l];
+        } else if constexpr (INV == 2) {
+          exact_div_small(r, a.d, a.d_inv32, a.p_inv_d, a.d_recip, a.w);
         }
         if (a.shift != 0u) rotr521(r, a.shift);
         if (a.out_fe) store_fe(tile_base(a.out_fe, tile), w, r);
@@ -326,20 +332,26 @@ extern "C" int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_
   std::memcpy(a.inv, w->inv, sizeof(a.inv));
   const dim3 g(grid_for(a.ntiles));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const bool inv = w->has_inv != 0;
-  switch (w->a_limbs) {
-    case 1:
-      if (inv) hipLaunchKernelGGL((reconstruct_kernel<1, true>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((reconstruct_kernel<1, false>), g, dim3(kBlock), 0, s, a);
-      break;
-    case 2:
-      if (inv) hipLaunchKernelGGL((reconstruct_kernel<2, true>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((reconstruct_kernel<2, false>), g, dim3(kBlock), 0, s, a);
-      break;
-    default:
-      if (inv) hipLaunchKernelGGL((reconstruct_kernel<17, true>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((reconstruct_kernel<17, false>), g, dim3(kBlock), 0, s, a);
-      break;
+  a.d = w->d;
+  a.d_inv32 = w->d_inv32;
+  a.p_inv_d = w->p_inv_d;
+  a.d_recip = w->d_recip;
+  std::memcpy(a.w, w->w, sizeof(a.w));
+  const int inv = w->has_inv;
+  if (inv < 0 || inv > 2 || (inv == 2 && (w->d < 3 || w->d >= 65536 || !(w->d & 1))))
+    return set_error(DN_ERR_ARG, "dn_m521_reconstruct: malformed divisor");
+#define DN_RECON(AL, IV) hipLaunchKernelGGL((reconstruct_kernel<AL, IV>), g, dim3(kBlock), 0, s, a)
+  switch (w->a_limbs * 4 + inv) {
+    case 1 * 4 + 0: DN_RECON(1, 0); break;
+    case 1 * 4 + 1: DN_RECON(1, 1); break;
+    case 1 * 4 + 2: DN_RECON(1, 2); break;
+    case 2 * 4 + 0: DN_RECON(2, 0); break;
+    case 2 * 4 + 1: DN_RECON(2, 1); break;
+    case 2 * 4 + 2: DN_RECON(2, 2); break;
+    case 17 * 4 + 0: DN_RECON(17, 0); break;
+    case 17 * 4 + 1: DN_RECON(17, 1); break;
+    default: DN_RECON(17, 2); break;
   }
+#undef DN_RECON
   return check_launch("dn_m521_reconstruct");
 }

@@ -49,9 +49,14 @@ class Lagrange(ctypes.Structure):
         ("neg", ctypes.c_uint32),
         ("shift", ctypes.c_int32),
         ("has_inv", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("d", ctypes.c_uint32),
         ("a", (ctypes.c_uint32 * 17) * MAX_RESOLVE),
         ("inv", ctypes.c_uint32 * 17),
+        ("d_inv32", ctypes.c_uint32),
+        ("p_inv_d", ctypes.c_uint32),
+        ("d_recip", ctypes.c_uint64),
+        ("w", ctypes.c_uint32 * 17),
+        ("reserved", ctypes.c_uint32),
     ]
 
 

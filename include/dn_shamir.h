@@ -89,19 +89,32 @@ int dn_m521_split_fe(const void* secrets_fe, const void* coeffs, void* shares,
 /*
  * Lagrange-at-0 weights for share abscissas xs[0..k-1], in the form the
  * reconstruct kernel consumes:  lambda_i = a_i / (d * 2^shift)  (mod p), with
- * |a_i| held in a_limbs little-endian u32 limbs, sign bit i of `neg`, and
- * inv = d^{-1} mod p when has_inv.  When the exact rationals do not fit, the
- * generic form is used: a_i = lambda_i mod p (a_limbs = 17), has_inv = 0.
+ * |a_i| held in a_limbs little-endian u32 limbs and the sign in bit i of `neg`.
+ * The division by d is
+ *   has_inv == 0: none (d == 1);
+ *   has_inv == 1: a multiplication by inv = d^{-1} mod p (full width);
+ *   has_inv == 2: an exact division by the small odd d (3 <= d < 2^16): the
+ *                 kernel adds m*p (m = -r * p^{-1} mod d, from r mod d via the
+ *                 residues w[i] = 2^(32 i) mod d and the reciprocal d_recip =
+ *                 floor((2^64-1)/d)) and divides limb by limb with d_inv32 =
+ *                 d^{-1} mod 2^32 — about a fifth of the full product's work.
+ * When the exact rationals do not fit, the generic form is used:
+ * a_i = lambda_i mod p (a_limbs = 17), has_inv = 0, shift = 0.
  */
 typedef struct dn_m521_lagrange {
-  int32_t k;                             /* number of shares, 1..16           */
-  int32_t a_limbs;                       /* 1, 2 or 17                        */
-  uint32_t neg;                          /* bit i set: a_i is negative        */
-  int32_t shift;                         /* 0..31: final division by 2^shift  */
-  int32_t has_inv;                       /* multiply by inv                   */
-  int32_t reserved;
+  int32_t k;                             /* number of shares, 1..16            */
+  int32_t a_limbs;                       /* 1, 2 or 17                         */
+  uint32_t neg;                          /* bit i set: a_i is negative         */
+  int32_t shift;                         /* 0..31: final division by 2^shift   */
+  int32_t has_inv;                       /* 0, 1 (multiply by inv), 2 (exact /d) */
+  uint32_t d;                            /* odd part of the denominator        */
   uint32_t a[DN_MAX_RESOLVE][DN_M521_LIMBS];
-  uint32_t inv[DN_M521_LIMBS];
+  uint32_t inv[DN_M521_LIMBS];           /* has_inv == 1: d^{-1} mod p         */
+  uint32_t d_inv32;                      /* has_inv == 2: d^{-1} mod 2^32      */
+  uint32_t p_inv_d;                      /* has_inv == 2: p^{-1} mod d         */
+  uint64_t d_recip;                      /* has_inv == 2: floor((2^64-1)/d)    */
+  uint32_t w[DN_M521_LIMBS];             /* has_inv == 2: 2^(32 i) mod d       */
+  uint32_t reserved;
 } dn_m521_lagrange_t;
 
 /* Host.  Validates like shamir.py:70-75 (k < threshold -> DN_ERR_TOO_FEW,

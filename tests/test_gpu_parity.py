@@ -233,6 +233,28 @@ def test_reconstruct_random_vs_c_oracle(xs):
             assert limbs_to_ints(got[e:e + 1])[0] == want
 
 
+@pytest.mark.parametrize("xs", [[2, 4, 5], [1, 2, 4, 5], [7, 100, 255], [2, 3, 5, 8, 9], [3, 5, 6, 11]])
+def test_reconstruct_exact_division_equals_full_inverse(xs, monkeypatch):
+    """has_inv == 2 (exact division by small odd d) vs has_inv == 1 (full
+    d^{-1} product): same canonical outputs, both equal to the C oracle."""
+    N = 1500
+    k = len(xs)
+    ys = c_oracle.draw_coeffs(77 + k, N, k).transpose(1, 0, 2).copy()
+    ys[:, :3, :] = 0
+    vecs = [torch.from_numpy(field.limbs_to_vec(ys[i])).to(dev()) for i in range(k)]
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DN_EXACT_DIV", mode)
+        w = _native.lagrange(xs, k)
+        res = torch.empty(field.vec_bytes(N), dtype=torch.uint8, device=dev())
+        _native.reconstruct(vecs, w, out_fe=res, n=N)
+        outs[(mode, w.has_inv)] = field.vec_to_limbs(res.cpu().numpy(), N)
+    assert {m for m, _ in outs} == {"1", "0"}
+    vals = list(outs.values())
+    assert np.array_equal(vals[0], vals[1])
+    assert np.array_equal(vals[0], c_oracle.reconstruct(ys, xs))
+
+
 def test_reconstruct_more_than_16_shares():
     N, n, t = 500, 20, 3
     sec = secrets_int64(5, N)

@@ -107,8 +107,15 @@ def _lam_from_desc(w):
     lams = []
     k = w.k
     scale = 1
-    if w.has_inv:
+    if w.has_inv == 1:
         scale = sum(w.inv[j] << (32 * j) for j in range(17))
+    elif w.has_inv == 2:
+        d = w.d
+        assert d % 2 == 1 and 3 <= d < 65536
+        assert (w.d_inv32 * d) % 2**32 == 1 and (w.p_inv_d * P) % d == 1
+        assert w.d_recip == (2**64 - 1) // d
+        assert [w.w[i] for i in range(17)] == [pow(2, 32 * i, d) for i in range(17)]
+        scale = op.inverse_mod(d, P)
     scale = scale * op.inverse_mod(pow(2, w.shift, P), P) % P
     for i in range(k):
         a = sum(w.a[i][j] << (32 * j) for j in range(w.a_limbs))
@@ -135,8 +142,16 @@ def test_lagrange_fast_forms():
     assert (w.a_limbs, w.has_inv, w.shift, w.neg) == (1, 0, 0, 0b010)
     w = _native.lagrange([1, 3, 5], 3)  # (15, -10, 3) / 8
     assert (w.a_limbs, w.has_inv, w.shift) == (1, 0, 3)
-    w = _native.lagrange([2, 4, 5], 3)  # (10, -15, 8) / 3
-    assert (w.a_limbs, w.has_inv, w.shift) == (1, 1, 0)
+    w = _native.lagrange([2, 4, 5], 3)  # (10, -15, 8) / 3: exact division by 3
+    assert (w.a_limbs, w.has_inv, w.shift, w.d) == (1, 2, 0, 3)
+
+
+def test_lagrange_full_inverse_form(monkeypatch):
+    monkeypatch.setenv("DN_EXACT_DIV", "0")
+    for xs in ([2, 4, 5], [1, 2, 4, 5], [7, 100, 255], [2, 3, 5, 8, 9]):
+        w = _native.lagrange(xs, 0)
+        assert w.has_inv in (0, 1)
+        assert _lam_from_desc(w) == _lam_ref(xs)
 
 
 def test_lagrange_errors_mirror_reference():
