@@ -94,12 +94,20 @@ __device__ __forceinline__ void canon(uint32_t v[kLimbs]) {
 }
 
 // Lazy v (< 2^544) -> canonical.  One fold (bits >= 521 added back at bit 0)
-// leaves v < 2^521 + 2^23, then canon().
+// leaves v < 2^521 + 2^23, then canon().  The fold's carry leaves limb 0 with
+// probability < 2^-9 and canon() has work only when limb 16 >= 0x1FF (same
+// odds), so both run behind branches that a wave skips unless one of its
+// lanes needs them (s_cbranch_execz): ~4 VALU ops in the common case.
 __device__ __forceinline__ void reduce(uint32_t v[kLimbs]) {
   const uint32_t hi = v[16] >> 9;
   v[16] &= kTopMask;
-  add_small(v, hi);
-  canon(v);
+  unsigned c;
+  v[0] = __builtin_addc(v[0], hi, 0u, &c);
+  if (__builtin_expect(c != 0u, 0)) {
+#pragma unroll
+    for (int i = 1; i < kLimbs; ++i) v[i] = __builtin_addc(v[i], 0u, c, &c);
+  }
+  if (__builtin_expect(v[16] >= kTopMask, 0)) canon(v);
 }
 
 // Lazy fold only: v (< 2^544) -> v' == v (mod p), v' < 2^521 + 2^23.
@@ -107,6 +115,57 @@ __device__ __forceinline__ void fold(uint32_t v[kLimbs]) {
   const uint32_t hi = v[16] >> 9;
   v[16] &= kTopMask;
   add_small(v, hi);
+}
+
+// v += u (17-limb add; caller guarantees no carry out of limb 16).
+__device__ __forceinline__ void add_fe(uint32_t v[kLimbs], const uint32_t u[kLimbs]) {
+  unsigned c = 0u;
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) v[i] = __builtin_addc(v[i], u[i], c, &c);
+}
+
+// D[k] += D[k+1] for k = 0..T-2 (one step of a forward-difference table),
+// the T-1 carry chains interleaved limb by limb.  Each chain's carry lives in
+// its own SGPR pair, so consecutive v_addc no longer depend on the carry the
+// previous VALU wrote (gfx950 needs 2 wait states for that: `s_nop 1` per limb
+// in a lone chain).  D[k+1] limb i is read before it is updated in the same
+// limb step, so the interleaving preserves the semantics.
+template <int T>
+__device__ __forceinline__ void fd_step(uint32_t D[T][kLimbs]) {
+  unsigned c[T > 1 ? T - 1 : 1];
+#pragma unroll
+  for (int k = 0; k + 1 < T; ++k) c[k] = 0u;
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) {
+#pragma unroll
+    for (int k = 0; k + 1 < T; ++k) D[k][i] = __builtin_addc(D[k][i], D[k + 1][i], c[k], &c[k]);
+  }
+}
+
+// Store f = D (lazy, < 2^544) as its canonical residue.  Common case (no
+// carry out of limb 0 after the fold, limb 16 < 0x1FF): the residue is D with
+// limb 0 += D >> 521 and limb 16 masked — stored straight from D's registers.
+// If any lane of the wave needs more (odds ~2^-9 per lane), the whole wave
+// takes the full reduce() on a copy (a wave-uniform branch on a ballot).
+__device__ __forceinline__ void store_reduced(uint8_t* __restrict__ tb, uint32_t w, const uint32_t D[kLimbs]) {
+  const uint32_t hi = D[16] >> 9;
+  const uint32_t top = D[16] & kTopMask;
+  unsigned c;
+  const uint32_t l0 = __builtin_addc(D[0], hi, 0u, &c);
+  const bool rare = (c != 0u) || (top == kTopMask);
+  if (__builtin_expect(__ballot(rare) != 0ull, 0)) {
+    uint32_t v[kLimbs];
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) v[i] = D[i];
+    reduce(v);
+    store_fe(tb, w, v);
+  } else {
+    const uint32_t o4 = w * 4u, o2 = w * 2u;
+    __builtin_nontemporal_store(l0, at<uint32_t>(tb, o4));
+#pragma unroll
+    for (int i = 1; i < 16; ++i) __builtin_nontemporal_store(D[i], at<uint32_t>(tb + i * 4 * kTile, o4));
+    __builtin_nontemporal_store(static_cast<uint16_t>(top), at<uint16_t>(tb + kHiOffset, o2));
+  }
 }
 
 // v = src * x + c   (x < 2^16, caller guarantees the result < 2^544).

@@ -54,9 +54,29 @@ __device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, u
   }
 }
 
-// T = compile-time threshold (1..8).  FOLD: fold after every Horner step
-// (needed when sum_{j<T} n^j >= 2^23, i.e. the unreduced value could pass
-// 2^544); otherwise only the final value is reduced.
+// Forward-difference matrix: Delta^k f(1) = sum_j M[k][j] c_j with
+// M[k][j] = Delta^k [x^j] at x = 1 = sum_i (-1)^(k-i) C(k,i) (1+i)^j
+// (e.g. t = 3: Delta^0 = c0+c1+c2, Delta^1 = c1+3c2, Delta^2 = 2c2).
+constexpr int64_t fd_coef(int k, int j) {
+  int64_t s = 0, binom = 1;
+  for (int i = 0; i <= k; ++i) {
+    int64_t pw = 1;
+    for (int e = 0; e < j; ++e) pw *= (1 + i);
+    s += (((k - i) & 1) ? -1 : 1) * binom * pw;
+    binom = binom * (k - i) / (i + 1);
+  }
+  return s;
+}
+
+// T = compile-time threshold (1..8).
+// FOLD == false: f(x) for x = 1..n by forward differences — the table
+// D_k = Delta^k f(x) (initialised from the coefficients with the small
+// constants above) advances with D_k += D_{k+1}: t-1 17-limb additions per
+// share, no multiplies.  Every D_k stays a non-negative integer below
+// 2^521 * sum_{j<t} (n+t)^j < 2^544 (checked on the host), so only the emitted
+// f(x) is reduced.
+// FOLD == true (large n or t): Horner per share (as _eval_at, shamir.py:19-25)
+// with a Mersenne fold after every step.
 template <int T, bool FE_SECRET, bool FOLD>
 __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -72,26 +92,58 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
       load_secret<FE_SECRET>(a, tile, w, c[0]);
 #pragma unroll
       for (int j = 1; j < T; ++j) load_fe(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.vec_bytes, tile), w, c[j]);
-#pragma unroll 1
-      for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
-        const uint32_t x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(xi));
-        uint32_t v[kLimbs];
-        if constexpr (T == 1) {
+      if constexpr (!FOLD) {
+        uint32_t D[T][kLimbs];
 #pragma unroll
-          for (int i = 0; i < kLimbs; ++i) v[i] = c[0][i];
-        } else {
-          mul_small_add(v, c[T - 1], x, c[T - 2]);
-          if constexpr (FOLD && T > 2) fold(v);
+        for (int k = 0; k < T; ++k) {
+          bool first = true;
 #pragma unroll
-          for (int j = T - 3; j >= 0; --j) {
-            mul_small_add(v, x, c[j]);
-            if constexpr (FOLD) {
-              if (j > 0) fold(v);
+          for (int j = T - 1; j >= k; --j) {
+            const int64_t m = fd_coef(k, j);
+            if (m == 0) continue;
+            if (first) {
+              if (m == 1) {
+#pragma unroll
+                for (int i = 0; i < kLimbs; ++i) D[k][i] = c[j][i];
+              } else {
+                uint32_t zero[kLimbs];
+#pragma unroll
+                for (int i = 0; i < kLimbs; ++i) zero[i] = 0u;
+                mul_small_add(D[k], c[j], static_cast<uint32_t>(m), zero);
+              }
+              first = false;
+            } else if (m == 1) {
+              add_fe(D[k], c[j]);
+            } else {
+              mul_small_add(D[k], c[j], static_cast<uint32_t>(m), D[k]);
             }
           }
         }
-        reduce(v);
-        store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, v);
+#pragma unroll 1
+        for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+          store_reduced(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, D[0]);
+          fd_step<T>(D);
+        }
+      } else {
+#pragma unroll 1
+        for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+          const uint32_t x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(xi));
+          uint32_t v[kLimbs];
+          if constexpr (T == 1) {
+#pragma unroll
+            for (int i = 0; i < kLimbs; ++i) v[i] = c[0][i];
+          } else {
+            mul_small_add(v, c[T - 1], x, c[T - 2]);
+            if constexpr (T > 2) fold(v);
+#pragma unroll
+            for (int j = T - 3; j >= 0; --j) {
+              mul_small_add(v, x, c[j]);
+              if (j > 0) fold(v);
+            }
+          }
+          reduce(v);
+          store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, v);
+        }
       }
     }
   }
@@ -155,7 +207,9 @@ struct ReconArgs {
 // for A = 17, a_i < p so < 2^1046), reduced once, then divided by d
 // (INV = 1: times d^{-1} mod p, a full product; INV = 2: exact division by a
 // small odd d) and by 2^shift (a 521-bit rotation).
-template <int A, int INV>
+// K > 0: compile-time share count — all K*17 loads of an element are issued
+// before the first multiply; K == 0: runtime count, one share at a time.
+template <int A, int INV, int K>
 __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) {
   constexpr int N = A + kLimbs;
   constexpr int VB = (A == kLimbs) ? 1046 : (521 + 32 * A + 4);
@@ -173,16 +227,31 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
         uint32_t S[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) S[i] = 0u;
-#pragma unroll 1
-        for (int32_t i = 0; i < a.k; ++i) {
-          uint32_t y[kLimbs];
-          load_fe(tile_base(a.shares[i], tile), w, y);
-          if ((a.neg >> i) & 1u) {  // -y == p - y == ~y within 521 bits
+        if constexpr (K > 0) {
+          uint32_t y[K][kLimbs];
 #pragma unroll
-            for (int l = 0; l < 16; ++l) y[l] = ~y[l];
-            y[16] = (~y[16]) & kTopMask;
+          for (int i = 0; i < K; ++i) load_fe(tile_base(a.shares[i], tile), w, y[i]);
+#pragma unroll
+          for (int i = 0; i < K; ++i) {
+            if ((a.neg >> i) & 1u) {  // -y == p - y == ~y within 521 bits
+#pragma unroll
+              for (int l = 0; l < 16; ++l) y[i][l] = ~y[i][l];
+              y[i][16] = (~y[i][16]) & kTopMask;
+            }
+            mac_wide<N, A>(S, a.a[i], y[i]);
           }
-          mac_wide<N, A>(S, a.a[i], y);
+        } else {
+#pragma unroll 1
+          for (int32_t i = 0; i < a.k; ++i) {
+            uint32_t y[kLimbs];
+            load_fe(tile_base(a.shares[i], tile), w, y);
+            if ((a.neg >> i) & 1u) {
+#pragma unroll
+              for (int l = 0; l < 16; ++l) y[l] = ~y[l];
+              y[16] = (~y[16]) & kTopMask;
+            }
+            mac_wide<N, A>(S, a.a[i], y);
+          }
         }
         uint32_t r[kLimbs];
         reduce_wide<N, VB>(S, r);
@@ -214,13 +283,34 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
   }
 }
 
-// Workgroups per launch: each 4-wave workgroup strides over tiles; 4096
-// workgroups = 16 per CU, enough waves to keep every CU's loads in flight.
+// DN_RECON_UNROLL=0 selects the runtime-k kernel (A/B hook, read per call).
+static bool recon_unroll() {
+  const char* e = std::getenv("DN_RECON_UNROLL");
+  return !(e && e[0] == '0');
+}
+
+template <int A, int INV>
+static void launch_recon_k(int k, dim3 g, hipStream_t s, const ReconArgs& a) {
+  if (A == 1 && recon_unroll()) {
+    switch (k) {
+      case 2: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 2>), g, dim3(kBlock), 0, s, a); return;
+      case 3: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 3>), g, dim3(kBlock), 0, s, a); return;
+      case 4: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 4>), g, dim3(kBlock), 0, s, a); return;
+      case 5: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 5>), g, dim3(kBlock), 0, s, a); return;
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((reconstruct_kernel<A, INV, 0>), g, dim3(kBlock), 0, s, a);
+}
+
+// Workgroups per launch: each 4-wave workgroup strides over tiles; up to
+// 16384 workgroups (2^24 elements: one tile per wave; measured 1-3 % ahead
+// of 4096 on reconstruct, profiles/r01/tune_gridcap*.jsonl).
 // DN_GRID_CAP overrides it (read per call; used by scripts/tune_kernels.py).
 static int grid_for(uint64_t ntiles) {
   const char* s = std::getenv("DN_GRID_CAP");
   const int v = s ? std::atoi(s) : 0;
-  const uint64_t cap = v > 0 ? static_cast<uint64_t>(v) : 4096u;
+  const uint64_t cap = v > 0 ? static_cast<uint64_t>(v) : 16384u;
   const uint64_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
   return static_cast<int>(blocks < cap ? blocks : cap);
 }
@@ -231,12 +321,13 @@ static int check_launch(const char* what) {
   return DN_OK;
 }
 
-// sum_{j<t} n^j < 2^23  <=>  the unreduced Horner value stays below 2^544.
+// Forward differences stay below 2^544 while sum_{j<t} (n+t)^j < 2^23
+// (every table entry is bounded by f at some x <= n + t - 1); otherwise fold.
 static bool needs_fold(int t, int n) {
   double s = 0.0, p = 1.0;
   for (int j = 0; j < t; ++j) {
     s += p;
-    p *= n;
+    p *= static_cast<double>(n + t);
   }
   return s >= 8388608.0;
 }
@@ -271,7 +362,9 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   a.threshold = threshold;
   const dim3 g(grid_for(a.ntiles));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const bool fold_each = needs_fold(threshold, n_shares);
+  // DN_SPLIT_HORNER=1 forces the Horner kernel (A/B hook, read per call).
+  const char* hz = std::getenv("DN_SPLIT_HORNER");
+  const bool fold_each = needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
   if (fe) {
     if (fold_each) launch_split_t<true, true>(threshold, g, s, a);
     else launch_split_t<true, false>(threshold, g, s, a);
@@ -340,7 +433,7 @@ extern "C" int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_
   const int inv = w->has_inv;
   if (inv < 0 || inv > 2 || (inv == 2 && (w->d < 3 || w->d >= 65536 || !(w->d & 1))))
     return set_error(DN_ERR_ARG, "dn_m521_reconstruct: malformed divisor");
-#define DN_RECON(AL, IV) hipLaunchKernelGGL((reconstruct_kernel<AL, IV>), g, dim3(kBlock), 0, s, a)
+#define DN_RECON(AL, IV) launch_recon_k<AL, IV>(w->k, g, s, a)
   switch (w->a_limbs * 4 + inv) {
     case 1 * 4 + 0: DN_RECON(1, 0); break;
     case 1 * 4 + 1: DN_RECON(1, 1); break;

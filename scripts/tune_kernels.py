@@ -42,16 +42,22 @@ def timeit(fn, iters=10):
     return s.elapsed_time(e) / iters
 
 
+unrolls = os.environ.get("UNROLLS", "1,0").split(",")
 for r in range(rounds):
-    for cap in caps:
+    for cap, unroll in [(c, u) for c in caps for u in unrolls]:
         os.environ["DN_GRID_CAP"] = str(cap)
-        t_split = timeit(lambda: _native.split_u64(sec, coeffs, shares, N, 3, 5))
-        res.setdefault((cap, "split"), []).append(t_split)
+        os.environ["DN_RECON_UNROLL"] = unroll
+        for horner in ("0", "1"):
+            os.environ["DN_SPLIT_HORNER"] = horner
+            t_split = timeit(lambda: _native.split_u64(sec, coeffs, shares, N, 3, 5))
+            res.setdefault((cap, "split_horner" if horner == "1" else "split_fd", unroll), []).append(t_split)
+        os.environ["DN_SPLIT_HORNER"] = "0"
         for name, (xs, rows) in configs.items():
             w = _native.lagrange(xs, 3)
             t_rec = timeit(lambda: _native.reconstruct([shares[i] for i in rows], w, out_u64=rec, n=N))
-            res.setdefault((cap, "rec" + name), []).append(t_rec)
-for (cap, kind), ts in sorted(res.items()):
-    b = N * (470 if kind == "split" else 206)
-    print(json.dumps({"cap": cap, "kernel": kind, "ms_median": float(np.median(ts)), "ms_min": float(np.min(ts)),
+            res.setdefault((cap, "rec" + name, unroll), []).append(t_rec)
+for (cap, kind, unroll), ts in sorted(res.items()):
+    b = N * (470 if kind.startswith("split") else 206)
+    print(json.dumps({"cap": cap, "kernel": kind, "recon_unroll": unroll, "ms_median": float(np.median(ts)),
+                      "ms_min": float(np.min(ts)),
                       "GBps_median": b / (np.median(ts) * 1e-3) / 1e9}))
