@@ -7,6 +7,7 @@
 * the reference's argument errors fire before any device work, and a device
   call without a HIP device raises (no CPU fallback).
 """
+import glob
 import os
 import random
 import re
@@ -23,21 +24,23 @@ from golden.fixtures import P, load_json, load_npz, manifest
 from oracle.py_shamir import RefSecretShare
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "dn_shamir.h")
+HEADERS = sorted(glob.glob(os.path.join(ROOT, "include", "*.h")))
 
 
 def header_symbols():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w ]+?\*?\s*\b(dn_\w+)\s*\(", text, re.M)))
 
 
 def test_library_exports_header_symbols():
+    from delta_node.utils import _mask_native
+
     syms = header_symbols()
-    assert len(syms) >= 8
+    assert len(syms) >= 13
     L = _native.lib()
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
-    assert sorted(_native.EXPORTS) == syms
+    assert sorted(_native.EXPORTS + _mask_native.EXPORTS) == syms
 
 
 def test_version_and_sizes():
