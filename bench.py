@@ -63,6 +63,52 @@ def cpu_baseline(t: int, n: int, xs, budget_s: float, max_elems: int) -> dict:
                       f"pure-Python restatement of delta_node/crypto/shamir, {dt:.1f} s on 1 core"}
 
 
+def rows_bench(dev, log2n: int) -> dict:
+    """SURVEY §8(f) rows measured beside the headline (device-resident inputs):
+    mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
+    pairwise masks (runner/horizontal/agg.py:284-318 with |u2| = 10)."""
+    import os as _os
+
+    from delta_node.utils import masked_sum
+    from oracle import py_mask as pm
+
+    n = 1 << log2n
+    val = torch.randn(n, dtype=torch.float64, device=dev) * 1e3
+    terms = [(_os.urandom(32), 1)] + [(_os.urandom(32), (-1) ** i) for i in range(9)]
+    out = torch.empty(n, dtype=torch.int64, device=dev)
+    masked_sum(val, terms, precision=8, out=out)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 5
+    s.record()
+    for _ in range(reps):
+        masked_sum(val, terms, precision=8, out=out)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    # parity on a prefix vs numpy (the reference's generator)
+    k = 1 << 14
+    vh = val[:k].cpu().numpy()
+    want = pm.fix_precision(vh, 8)
+    for sd, sg in terms:
+        want = want + sg * pm.make_mask_numpy(sd, (k,))  # a prefix of the length-n mask
+    ok = bool(np.array_equal(out[:k].cpu().numpy(), want))
+    # CPU baseline: the reference's numpy calls on a 2^20 sample, 1 thread of numpy
+    m = 1 << 20
+    vs = np.random.default_rng(0).standard_normal(m) * 1e3
+    t0 = time.perf_counter()
+    acc = pm.fix_precision(vs, 8)
+    for sd, sg in terms:
+        acc = acc + sg * pm.make_mask_numpy(sd, vs.shape)
+    cpu_dt = time.perf_counter() - t0
+    return {"mask_masking": {
+        "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
+        "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
+        "hbm_GBps": 16 * n / (ms * 1e-3) / 1e9, "bound": "valu (PCG64 128-bit LCG + Lemire per draw)",
+        "numpy_prefix_equal": ok,
+        "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}}
+
+
 def load_traffic(path: str):
     try:
         with open(path) as f:
@@ -82,6 +128,7 @@ def main():
     ap.add_argument("--xs", type=str, default="1,3,5")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline sampling (0 = skip)")
     ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of share blocks (N>1)")
+    ap.add_argument("--rows", type=int, default=1, help="also measure the SURVEY §8(f) rows built so far")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -214,6 +261,8 @@ def main():
     }
     if allgather:
         line["allgather"] = allgather
+    if args.rows:
+        line["rows"] = rows_bench(dev, args.log2n)
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         line["cpu_baseline"] = cpu_baseline(t, n, xs, args.cpu_budget, 1 << 20)
     if rank == 0:

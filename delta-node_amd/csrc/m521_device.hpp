@@ -67,6 +67,32 @@ __device__ __forceinline__ void store_fe(uint8_t* __restrict__ tb, uint32_t w, c
   __builtin_nontemporal_store(static_cast<uint16_t>(v[16]), at<uint16_t>(tb + kHiOffset, o2));
 }
 
+// ---- buffer-resource addressing (cdna guide T8/T20) --------------------------
+// One 128-bit descriptor per (vector, tile), built from wave-uniform values in
+// SGPRs; each lane then needs a single 32-bit VGPR offset (w * 4) for all 17
+// limb accesses, the limb's byte offset riding in soffset.  aux = 2: nt.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kNt = 2;
+
+__device__ __forceinline__ rsrc_t tile_rsrc(const uint8_t* tb) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(tb), 0, static_cast<int>(kTileBytes), 0x00020000);
+}
+
+__device__ __forceinline__ void load_fe_b(rsrc_t r, uint32_t w, uint32_t v[kLimbs]) {
+  const uint32_t o4 = w * 4u, o2 = w * 2u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b32(r, o4, i * 4 * kTile, kNt);
+  v[16] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b16(r, o2, static_cast<int>(kHiOffset), kNt)) &
+          kTopMask;
+}
+
+__device__ __forceinline__ void store_fe_b(rsrc_t r, uint32_t w, const uint32_t v[kLimbs]) {
+  const uint32_t o4 = w * 4u, o2 = w * 2u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) __builtin_amdgcn_raw_buffer_store_b32(v[i], r, o4, i * 4 * kTile, kNt);
+  __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(v[16]), r, o2, static_cast<int>(kHiOffset), kNt);
+}
+
 // ---- carry chains ----------------------------------------------------------
 // v += s (s a small u32), ripple through all limbs.
 __device__ __forceinline__ void add_small(uint32_t v[kLimbs], uint32_t s) {
@@ -146,25 +172,23 @@ __device__ __forceinline__ void fd_step(uint32_t D[T][kLimbs]) {
 // carry out of limb 0 after the fold, limb 16 < 0x1FF): the residue is D with
 // limb 0 += D >> 521 and limb 16 masked — stored straight from D's registers.
 // If any lane of the wave needs more (odds ~2^-9 per lane), the whole wave
-// takes the full reduce() on a copy (a wave-uniform branch on a ballot).
-__device__ __forceinline__ void store_reduced(uint8_t* __restrict__ tb, uint32_t w, const uint32_t D[kLimbs]) {
+// reduces D IN PLACE (same residue, smaller value: later forward differences
+// stay exact and within bounds) and stores it — no copy, no extra registers.
+__device__ __forceinline__ void store_reduced(rsrc_t r, uint32_t w, uint32_t D[kLimbs]) {
   const uint32_t hi = D[16] >> 9;
   const uint32_t top = D[16] & kTopMask;
   unsigned c;
   const uint32_t l0 = __builtin_addc(D[0], hi, 0u, &c);
   const bool rare = (c != 0u) || (top == kTopMask);
   if (__builtin_expect(__ballot(rare) != 0ull, 0)) {
-    uint32_t v[kLimbs];
-#pragma unroll
-    for (int i = 0; i < kLimbs; ++i) v[i] = D[i];
-    reduce(v);
-    store_fe(tb, w, v);
+    reduce(D);
+    store_fe_b(r, w, D);
   } else {
     const uint32_t o4 = w * 4u, o2 = w * 2u;
-    __builtin_nontemporal_store(l0, at<uint32_t>(tb, o4));
+    __builtin_amdgcn_raw_buffer_store_b32(l0, r, o4, 0, kNt);
 #pragma unroll
-    for (int i = 1; i < 16; ++i) __builtin_nontemporal_store(D[i], at<uint32_t>(tb + i * 4 * kTile, o4));
-    __builtin_nontemporal_store(static_cast<uint16_t>(top), at<uint16_t>(tb + kHiOffset, o2));
+    for (int i = 1; i < 16; ++i) __builtin_amdgcn_raw_buffer_store_b32(D[i], r, o4, i * 4 * kTile, kNt);
+    __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(top), r, o2, static_cast<int>(kHiOffset), kNt);
   }
 }
 

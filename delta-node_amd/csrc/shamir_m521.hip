@@ -43,7 +43,7 @@ constexpr int kWavesPerBlock = kBlock / 64;
 template <bool FE_SECRET>
 __device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, uint32_t w, uint32_t c0[kLimbs]) {
   if constexpr (FE_SECRET) {
-    load_fe(tile_base(a.sec_fe, tile), w, c0);
+    load_fe_b(tile_rsrc(tile_base(a.sec_fe, tile)), w, c0);
   } else {
     const int64_t* sec = a.sec_u64 + static_cast<uint64_t>(tile) * kTile;  // uniform base
     const uint64_t s = static_cast<uint64_t>(__builtin_nontemporal_load(sec + w));
@@ -54,25 +54,19 @@ __device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, u
   }
 }
 
-// Forward-difference matrix: Delta^k f(1) = sum_j M[k][j] c_j with
-// M[k][j] = Delta^k [x^j] at x = 1 = sum_i (-1)^(k-i) C(k,i) (1+i)^j
-// (e.g. t = 3: Delta^0 = c0+c1+c2, Delta^1 = c1+3c2, Delta^2 = 2c2).
-constexpr int64_t fd_coef(int k, int j) {
-  int64_t s = 0, binom = 1;
-  for (int i = 0; i <= k; ++i) {
-    int64_t pw = 1;
-    for (int e = 0; e < j; ++e) pw *= (1 + i);
-    s += (((k - i) & 1) ? -1 : 1) * binom * pw;
-    binom = binom * (k - i) / (i + 1);
-  }
-  return s;
+// D = 2 * c (a one-bit left shift across limbs; c < 2^521 so no overflow).
+__device__ __forceinline__ void twice(uint32_t D[kLimbs], const uint32_t c[kLimbs]) {
+#pragma unroll
+  for (int i = kLimbs - 1; i > 0; --i) D[i] = __builtin_amdgcn_alignbit(c[i], c[i - 1], 31);
+  D[0] = c[0] << 1;
 }
+
+constexpr int64_t fd_factorial(int k) { return k <= 1 ? 1 : k * fd_factorial(k - 1); }
 
 // T = compile-time threshold (1..8).
 // FOLD == false: f(x) for x = 1..n by forward differences — the table
-// D_k = Delta^k f(x) (initialised from the coefficients with the small
-// constants above) advances with D_k += D_{k+1}: t-1 17-limb additions per
-// share, no multiplies.  Every D_k stays a non-negative integer below
+// D_k = Delta^k f(x) (built in place from the coefficients, below) advances
+// with D_k += D_{k+1}: t-1 17-limb additions per share, no multiplies.  Every D_k stays a non-negative integer below
 // 2^521 * sum_{j<t} (n+t)^j < 2^544 (checked on the host), so only the emitted
 // f(x) is reduced.
 // FOLD == true (large n or t): Horner per share (as _eval_at, shamir.py:19-25)
@@ -91,37 +85,52 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
       uint32_t c[T][kLimbs];
       load_secret<FE_SECRET>(a, tile, w, c[0]);
 #pragma unroll
-      for (int j = 1; j < T; ++j) load_fe(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.vec_bytes, tile), w, c[j]);
+      for (int j = 1; j < T; ++j)
+        load_fe_b(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.vec_bytes, tile)), w, c[j]);
       if constexpr (!FOLD) {
-        uint32_t D[T][kLimbs];
+        // In place, c becomes the forward-difference table at x = 1:
+        // synthetic division by (x - z) for z = 1..T-1 turns the monomial
+        // coefficients into Newton coefficients b_k on nodes 1, 2, ...
+        // (f = b0 + b1 (x-1) + b2 (x-1)(x-2) + ...), and Delta^k f(1) = k! b_k.
+        // Every step is c[j] += z * c[j+1] with a small constant z.
+        if constexpr (T == 3) {
+          // hand-ordered for the headline t = 3 (58 VGPRs, 8 waves/SIMD):
+          // D2 = 2 c2; c2 <- c1 + c2; c1 <- c2 + D2 (= c1 + 3 c2); c2 <- c2 + c0.
+          uint32_t d2[kLimbs];
+          twice(d2, c[2]);
+          add_fe(c[2], c[1]);
 #pragma unroll
-        for (int k = 0; k < T; ++k) {
-          bool first = true;
+          for (int i = 0; i < kLimbs; ++i) c[1][i] = c[2][i];
+          add_fe(c[1], d2);
+          add_fe(c[2], c[0]);
 #pragma unroll
-          for (int j = T - 1; j >= k; --j) {
-            const int64_t m = fd_coef(k, j);
-            if (m == 0) continue;
-            if (first) {
-              if (m == 1) {
+          for (int i = 0; i < kLimbs; ++i) {
+            c[0][i] = c[2][i];
+            c[2][i] = d2[i];
+          }
+        } else {
 #pragma unroll
-                for (int i = 0; i < kLimbs; ++i) D[k][i] = c[j][i];
-              } else {
-                uint32_t zero[kLimbs];
+          for (int k = 0; k + 1 < T; ++k) {
 #pragma unroll
-                for (int i = 0; i < kLimbs; ++i) zero[i] = 0u;
-                mul_small_add(D[k], c[j], static_cast<uint32_t>(m), zero);
-              }
-              first = false;
-            } else if (m == 1) {
-              add_fe(D[k], c[j]);
-            } else {
-              mul_small_add(D[k], c[j], static_cast<uint32_t>(m), D[k]);
+            for (int j = T - 2; j >= k; --j) {
+              if (k == 0) add_fe(c[j], c[j + 1]);
+              else mul_small_add(c[j], c[j + 1], static_cast<uint32_t>(k + 1), c[j]);
+            }
+          }
+          if constexpr (T >= 3) {
+#pragma unroll
+            for (int k = 2; k < T; ++k) {
+              uint32_t zero[kLimbs];
+#pragma unroll
+              for (int i = 0; i < kLimbs; ++i) zero[i] = 0u;
+              mul_small_add(c[k], c[k], static_cast<uint32_t>(fd_factorial(k)), zero);
             }
           }
         }
+        uint32_t (&D)[T][kLimbs] = c;
 #pragma unroll 1
         for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
-          store_reduced(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, D[0]);
+          store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile)), w, D[0]);
           fd_step<T>(D);
         }
       } else {
@@ -142,7 +151,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
             }
           }
           reduce(v);
-          store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, v);
+          store_fe_b(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile)), w, v);
         }
       }
     }
@@ -322,7 +331,8 @@ static int check_launch(const char* what) {
 }
 
 // Forward differences stay below 2^544 while sum_{j<t} (n+t)^j < 2^23
-// (every table entry is bounded by f at some x <= n + t - 1); otherwise fold.
+// (every table entry, and every intermediate Newton coefficient, is bounded by
+// f at some x <= n + t - 1); otherwise fold.
 static bool needs_fold(int t, int n) {
   double s = 0.0, p = 1.0;
   for (int j = 0; j < t; ++j) {
