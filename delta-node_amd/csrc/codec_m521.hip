@@ -1,0 +1,268 @@
+// codec_m521.hip — the share wire codec over whole vectors.
+//
+// Reference (delta_node/crypto/shamir/shamir.py:28-45, serialize/hex.py:44-50):
+//   _share_to_bytes((x, y)) = bytes([len(xb)]) + xb + yb,
+//   xb / yb = minimal big-endian bytes (0 -> b"").
+// The vector form encodes share x of every element into one packed byte
+// stream (records back to back) plus int64 offsets[n + 1]; record e is
+// exactly the reference's bytes for (x, y_e).  Decoding parses records back
+// into a tiled vector (and each record's x).
+//
+// Encode = three launches: (1) per 1024-element block: record lengths and
+// their in-block exclusive scan, block total; (2) scan of the block totals;
+// (3) per wave: records assembled in LDS at their final byte positions
+// (mod 4 aligned like the destination), then written out as aligned dwords
+// plus a few head/tail bytes, so global writes stay contiguous and wide.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "dn_internal.hpp"
+#include "m521_device.hpp"
+
+namespace dn {
+
+constexpr int kCodecBlock = 256;
+constexpr int kScanElems = 1024;       // elements per scan block (4 per thread)
+constexpr int kMaxRecord = 1 + 8 + 66;  // [len][x up to 8 bytes][y up to 66 bytes]
+
+struct XBytes {
+  uint32_t len;
+  uint8_t b[8];  // big-endian minimal bytes of x
+};
+
+// Minimal big-endian byte length of a canonical 17-limb value (0 -> 0).
+__device__ __forceinline__ uint32_t y_len(const uint32_t v[kLimbs]) {
+  uint32_t len = 0;
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) {
+    if (v[i]) len = 4u * i + (32u - __builtin_clz(v[i]) + 7u) / 8u;
+  }
+  return len;
+}
+
+// Same, reading only as many limbs as needed from the top: limb 16 (the u16
+// plane) is non-zero with odds 1 - 2^-9 for a uniform residue, so the length
+// pass usually reads 2 of the 66 bytes.
+__device__ __forceinline__ uint32_t y_len_mem(const uint8_t* vec, uint64_t e) {
+  const uint8_t* tb = tile_base(vec, static_cast<uint32_t>(e / kTile));
+  const uint32_t w = static_cast<uint32_t>(e % kTile);
+  const uint32_t top = reinterpret_cast<const uint16_t*>(tb + kHiOffset)[w] & kTopMask;
+  if (top) return 64u + (32u - __builtin_clz(top) + 7u) / 8u;
+  for (int i = 15; i >= 0; --i) {
+    const uint32_t l = reinterpret_cast<const uint32_t*>(tb)[i * kTile + w];
+    if (l) return 4u * i + (32u - __builtin_clz(l) + 7u) / 8u;
+  }
+  return 0u;
+}
+
+__global__ void __launch_bounds__(kCodecBlock) lengths_scan_kernel(const uint8_t* __restrict__ vec, uint64_t n,
+                                                                    uint32_t xlen, uint32_t* __restrict__ local,
+                                                                    uint64_t* __restrict__ block_tot) {
+  __shared__ uint32_t s_sum[kCodecBlock];
+  const uint64_t b = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  uint32_t len[4], sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t e = b * kScanElems + t * 4 + j;
+    len[j] = 0;
+    if (e < n) len[j] = 1u + xlen + y_len_mem(vec, e);
+    sum += len[j];
+  }
+  s_sum[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < kCodecBlock; off <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t add = t >= static_cast<uint32_t>(off) ? s_sum[t - off] : 0u;
+    __syncthreads();
+    s_sum[t] += add;
+    __syncthreads();
+  }
+  uint32_t run = s_sum[t] - sum;  // exclusive prefix of this thread's 4 elements
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t e = b * kScanElems + t * 4 + j;
+    if (e < n) local[e] = run;
+    run += len[j];
+  }
+  if (t == kCodecBlock - 1) block_tot[b] = s_sum[t];
+}
+
+// Exclusive scan of the block totals in one workgroup (nb <= a few 10^5).
+__global__ void __launch_bounds__(1024) scan_blocks_kernel(uint64_t* __restrict__ tot, uint64_t nb,
+                                                           uint64_t* __restrict__ total_out) {
+  __shared__ uint64_t s[1024];
+  const uint32_t t = threadIdx.x;
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t lo = t * per, hi = lo + per < nb ? lo + per : nb;
+  uint64_t sum = 0;
+  for (uint64_t i = lo; i < hi; ++i) sum += tot[i];
+  s[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const uint64_t add = t >= static_cast<uint32_t>(off) ? s[t - off] : 0ull;
+    __syncthreads();
+    s[t] += add;
+    __syncthreads();
+  }
+  uint64_t run = s[t] - sum;
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t v = tot[i];
+    tot[i] = run;
+    run += v;
+  }
+  if (t == 1023) *total_out = s[1023];
+}
+
+// One wave = 64 consecutive elements = one contiguous run of records.
+__global__ void __launch_bounds__(kCodecBlock) encode_kernel(const uint8_t* __restrict__ vec, uint64_t n, XBytes xb,
+                                                             const uint32_t* __restrict__ local,
+                                                             const uint64_t* __restrict__ block_pre,
+                                                             uint64_t* __restrict__ offsets, uint8_t* __restrict__ out) {
+  __shared__ uint32_t s_buf[kCodecBlock / 64][(64 * kMaxRecord + 8) / 4 + 1];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t e = (static_cast<uint64_t>(blockIdx.x) * kCodecBlock) + threadIdx.x;
+  const bool valid = e < n;
+  const uint64_t vmask = __ballot(valid);
+  if (!vmask) return;  // wave-uniform: the whole wave is past the end
+  uint32_t v[kLimbs];
+  uint64_t off = 0;
+  uint32_t ylen = 0;
+  if (valid) {
+    load_fe(tile_base(vec, static_cast<uint32_t>(e / kTile)), static_cast<uint32_t>(e % kTile), v);
+    ylen = y_len(v);
+    off = block_pre[e / kScanElems] + local[e];
+    offsets[e] = off;
+    if (e == n - 1) offsets[n] = off + 1 + xb.len + ylen;
+  }
+  // the wave's byte range [A, B)
+  const uint64_t A = __shfl(off, 0);
+  const uint32_t last = static_cast<uint32_t>(63 - __builtin_clzll(vmask));
+  const uint64_t endl = off + (valid ? 1 + xb.len + ylen : 0);
+  const uint64_t B = __shfl(endl, last);
+  const uint64_t A4 = A & ~3ull;
+  uint8_t* sb = reinterpret_cast<uint8_t*>(s_buf[wv]);
+  if (valid) {
+    uint32_t p = static_cast<uint32_t>(off - A4);
+    sb[p++] = static_cast<uint8_t>(xb.len);
+    for (uint32_t i = 0; i < xb.len; ++i) sb[p++] = xb.b[i];
+    for (int i = static_cast<int>(ylen) - 1; i >= 0; --i) sb[p++] = static_cast<uint8_t>(v[i >> 2] >> (8 * (i & 3)));
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // head bytes [A, a4), aligned body [a4, b4), tail [b4, B)
+  const uint64_t a4 = (A + 3) & ~3ull, b4 = B & ~3ull;
+  if (a4 > b4) {  // the whole range sits inside one dword
+    for (uint64_t q = A + lane; q < B; q += 64) out[q] = sb[q - A4];
+    return;
+  }
+  if (lane < a4 - A) out[A + lane] = sb[A + lane - A4];
+  if (lane < B - b4) out[b4 + lane] = sb[b4 + lane - A4];
+  const uint32_t* sw = s_buf[wv];
+  uint32_t* ow = reinterpret_cast<uint32_t*>(out + a4);
+  const uint32_t base_w = static_cast<uint32_t>((a4 - A4) / 4);
+  const uint32_t nw = static_cast<uint32_t>((b4 - a4) / 4);
+  for (uint32_t q = lane; q < nw; q += 64) __builtin_nontemporal_store(sw[base_w + q], ow + q);
+}
+
+// Decode record e -> element e of a tiled vector (+ its x).  y is reduced
+// mod p (resolve_shares reduces ys the same way, shamir.py:86-88).  Records
+// whose y has more than 68 significant bytes, or whose x is longer than
+// 8 bytes, are counted in *bad and stored as 0 (the caller re-decodes them).
+__global__ void __launch_bounds__(kCodecBlock) decode_kernel(const uint8_t* __restrict__ in,
+                                                             const uint64_t* __restrict__ offsets, uint64_t n,
+                                                             uint8_t* __restrict__ vec, uint64_t* __restrict__ xs,
+                                                             uint32_t* __restrict__ bad) {
+  const uint64_t e = (static_cast<uint64_t>(blockIdx.x) * kCodecBlock) + threadIdx.x;
+  if (e >= n) return;
+  const uint64_t o = offsets[e], end = offsets[e + 1];
+  bool ok = end > o;
+  const uint32_t xlen = ok ? in[o] : 0u;
+  uint64_t x = 0;
+  ok = ok && xlen <= 8 && o + 1 + xlen <= end;
+  if (ok)
+    for (uint32_t i = 0; i < xlen; ++i) x = (x << 8) | in[o + 1 + i];
+  uint32_t v[kLimbs];
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) v[i] = 0u;
+  if (ok) {
+    const uint64_t y0 = o + 1 + xlen;
+    uint64_t skip = 0;  // leading zero bytes are allowed (bytes_to_int ignores them)
+    while (y0 + skip < end && in[y0 + skip] == 0) ++skip;
+    const uint64_t sig = end - y0 - skip;
+    ok = sig <= 68;
+    if (ok) {
+      for (uint64_t i = 0; i < sig; ++i) {
+        const uint32_t byte = in[end - 1 - i];
+        v[i >> 2] |= byte << (8 * (i & 3));
+      }
+      reduce(v);
+    }
+  }
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) v[i] = 0u;
+    atomicAdd(bad, 1u);
+  }
+  store_fe(tile_base(vec, static_cast<uint32_t>(e / kTile)), static_cast<uint32_t>(e % kTile), v);
+  if (xs) xs[e] = x;
+}
+
+}  // namespace dn
+
+using namespace dn;
+
+extern "C" uint64_t dn_m521_codec_scratch_bytes(uint64_t n_elem) {
+  const uint64_t nb = (n_elem + kScanElems - 1) / kScanElems;
+  return n_elem * 4 + nb * 8 + 8 + 256;
+}
+
+extern "C" uint64_t dn_m521_encoded_capacity(uint64_t n_elem, uint64_t x) {
+  uint32_t xl = 0;
+  while (xl < 8 && (x >> (8 * xl))) ++xl;
+  return n_elem * (1 + xl + 66);
+}
+
+extern "C" int dn_m521_encode_shares(const void* vec, uint64_t n_elem, uint64_t x, uint64_t* offsets, uint8_t* out,
+                                     uint64_t capacity, void* scratch, uint64_t scratch_bytes, void* stream) {
+  if (n_elem == 0) return DN_OK;
+  if (!vec || !offsets || !out || !scratch) return set_error(DN_ERR_ARG, "dn_m521_encode_shares: null pointer");
+  if (capacity < dn_m521_encoded_capacity(n_elem, x))
+    return set_error(DN_ERR_ARG, "dn_m521_encode_shares: capacity %llu < %llu", (unsigned long long)capacity,
+                     (unsigned long long)dn_m521_encoded_capacity(n_elem, x));
+  if (scratch_bytes < dn_m521_codec_scratch_bytes(n_elem))
+    return set_error(DN_ERR_ARG, "dn_m521_encode_shares: scratch too small");
+  XBytes xb;
+  std::memset(&xb, 0, sizeof(xb));
+  while (xb.len < 8 && (x >> (8 * xb.len))) ++xb.len;
+  for (uint32_t i = 0; i < xb.len; ++i) xb.b[i] = static_cast<uint8_t>(x >> (8 * (xb.len - 1 - i)));
+  const uint64_t nb = (n_elem + kScanElems - 1) / kScanElems;
+  uint32_t* local = static_cast<uint32_t*>(scratch);
+  uint64_t* tot = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(scratch) + ((n_elem * 4 + 15) & ~15ull));
+  uint64_t* total = tot + nb;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint8_t* v = static_cast<const uint8_t*>(vec);
+  hipLaunchKernelGGL(lengths_scan_kernel, dim3(static_cast<uint32_t>(nb)), dim3(kCodecBlock), 0, s, v, n_elem,
+                     xb.len, local, tot);
+  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, s, tot, nb, total);
+  const uint64_t blocks = (n_elem + kCodecBlock - 1) / kCodecBlock;
+  hipLaunchKernelGGL(encode_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0, s, v, n_elem, xb,
+                     local, tot, offsets, out);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_m521_encode_shares: %s", hipGetErrorString(err));
+  return DN_OK;
+}
+
+extern "C" int dn_m521_decode_shares(const uint8_t* in, const uint64_t* offsets, uint64_t n_elem, void* vec,
+                                     uint64_t* xs, uint32_t* bad_count, void* stream) {
+  if (n_elem == 0) return DN_OK;
+  if (!in || !offsets || !vec || !bad_count) return set_error(DN_ERR_ARG, "dn_m521_decode_shares: null pointer");
+  const uint64_t blocks = (n_elem + kCodecBlock - 1) / kCodecBlock;
+  hipLaunchKernelGGL(decode_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0,
+                     static_cast<hipStream_t>(stream), in, offsets, n_elem, static_cast<uint8_t*>(vec), xs,
+                     bad_count);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_m521_decode_shares: %s", hipGetErrorString(err));
+  return DN_OK;
+}

@@ -149,6 +149,28 @@ int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_lagrange_t*
 int dn_mt19937_draw_coeffs(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem,
                            int tm1, void* coeffs);
 
+/*
+ * Share wire codec over whole vectors (shamir.py:28-45 `_share_to_bytes` /
+ * `_bytes_to_share`, serialize/hex.py:44-50).  Record e of the packed stream
+ * is exactly the reference's bytes for share (x, y_e):
+ *     [len(xb)][xb][yb],  xb / yb minimal big-endian (0 -> empty)
+ * and records are back to back: record e = out[offsets[e] : offsets[e+1]].
+ */
+/* Device scratch bytes dn_m521_encode_shares needs for n elements. */
+uint64_t dn_m521_codec_scratch_bytes(uint64_t n_elem);
+/* Upper bound of the packed size (n * (1 + len(xb) + 66)): size `out` to this. */
+uint64_t dn_m521_encoded_capacity(uint64_t n_elem, uint64_t x);
+/* Encode share x of a tiled vector: device uint64 offsets[n+1], device out
+ * (capacity >= dn_m521_encoded_capacity), device scratch. */
+int dn_m521_encode_shares(const void* vec, uint64_t n_elem, uint64_t x, uint64_t* offsets, uint8_t* out,
+                          uint64_t capacity, void* scratch, uint64_t scratch_bytes, void* stream);
+/* Decode records (device in, offsets[n+1]) into a tiled vector, y reduced
+ * mod p as resolve_shares does; xs (device uint64[n], may be NULL) receives
+ * each record's x.  Records with x longer than 8 bytes or y longer than 68
+ * bytes are counted in *bad_count (device) and decoded as 0. */
+int dn_m521_decode_shares(const uint8_t* in, const uint64_t* offsets, uint64_t n_elem, void* vec, uint64_t* xs,
+                          uint32_t* bad_count, void* stream);
+
 /* Thread-local message of the last failure (never NULL). */
 const char* dn_last_error(void);
 

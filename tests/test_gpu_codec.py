@@ -1,0 +1,98 @@
+"""HIP share wire codec vs the reference's bytes.
+
+The packed records must equal, byte for byte, the `_share_to_bytes` output
+the reference produced for the same shares (tests/golden f1/f2/f3, generated
+from delta_node/crypto/shamir/shamir.py), and decoding must give back the
+share vectors.  Larger and edge-case vectors are checked against a host
+encoding with the reference's own codec restated (oracle/py_shamir.py).
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from delta_node.crypto import shamir
+from delta_node.crypto.shamir import codec, field
+from golden.fixtures import P, load_json, load_npz, manifest, unpack_share_bytes
+from oracle.py_shamir import share_to_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def dev():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+@pytest.mark.parametrize("key", ["f1", "f2"])
+def test_encode_matches_reference_share_bytes(key):
+    cfg = manifest()[key]
+    z = load_npz(cfg["file"])
+    N, n, t = cfg["N"], cfg["n"], cfg["t"]
+    ss = shamir.SecretShare(t)
+    ss.random.seed(cfg["mt_seed"])
+    block = ss.make_shares_vec(torch.from_numpy(z["secrets"]), n)
+    for x in range(1, n + 1):
+        packed, offs = codec.encode_share_vec(block[x - 1], N, x)
+        recs = codec.records_to_list(packed.cpu(), offs.cpu())
+        want = [unpack_share_bytes(z["share_bytes"], z["share_offsets"], e * n + x - 1) for e in range(N)]
+        assert recs == want, x
+        assert bytes(packed.cpu().numpy()) == b"".join(want)
+        vec, xs = codec.decode_share_vec(packed, offs, N)
+        assert torch.equal(vec[: field.vec_bytes(N)], block[x - 1]) or np.array_equal(
+            field.vec_to_limbs(vec.cpu().numpy(), N), field.vec_to_limbs(block[x - 1].cpu().numpy(), N))
+        assert torch.all(xs == x)
+
+
+def test_encode_edge_values_and_wide_x():
+    vals = [0, 1, 255, 256, 2**64 - 1, 2**512, P - 1, 2**520, 2**519 + 5, 7 << 300] + \
+        [random.Random(i).randrange(P) for i in range(300)]
+    n = len(vals)
+    vec = torch.from_numpy(field.ints_to_vec(vals)).to(dev())
+    for x in (1, 5, 255, 256, 300, 65535, 2**40 + 3):
+        packed, offs = codec.encode_share_vec(vec, n, x)
+        recs = codec.records_to_list(packed.cpu(), offs.cpu())
+        assert recs == [share_to_bytes(x, y) for y in vals], x
+        back, xs = codec.decode_share_vec(packed, offs, n)
+        assert field.vec_to_ints(back.cpu().numpy(), n) == vals
+        assert torch.all(xs == x)
+
+
+@pytest.mark.parametrize("n", [1, 255, 1023, 1024, 1025, 70001])
+def test_encode_ragged_random_vs_host(n):
+    rng = random.Random(n)
+    vals = [rng.randrange(P) >> rng.randrange(0, 521) for _ in range(n)]  # many byte lengths
+    vec = torch.from_numpy(field.ints_to_vec(vals)).to(dev())
+    packed, offs = codec.encode_share_vec(vec, n, 3)
+    want = b"".join(share_to_bytes(3, y) for y in vals)
+    assert bytes(packed.cpu().numpy()) == want
+    assert int(offs[n].item()) == len(want)
+    back, _ = codec.decode_share_vec(packed, offs, n)
+    assert field.vec_to_ints(back.cpu().numpy(), n) == vals
+
+
+def test_decode_reduces_like_resolve_and_flags_oversize():
+    """Records as a peer might send them: leading zero bytes, y >= p (reduced
+    mod p as resolve_shares does, shamir.py:86-88), oversize y (flagged)."""
+    ys = [0, 5, P, P + 9, (1 << 527) + 1]
+    recs = [bytes([1, 2]) + b"\x00\x00" + (5).to_bytes(1, "big")] + \
+           [share_to_bytes(2, y) for y in ys]
+    packed = torch.tensor(list(b"".join(recs)), dtype=torch.uint8, device=dev())
+    offs = torch.tensor(np.cumsum([0] + [len(r) for r in recs]), dtype=torch.int64, device=dev())
+    vec, xs = codec.decode_share_vec(packed, offs, len(recs))
+    assert field.vec_to_ints(vec.cpu().numpy(), len(recs)) == [5] + [y % P for y in ys]
+    bad = torch.tensor(list(share_to_bytes(2, 1 << 560)), dtype=torch.uint8, device=dev())
+    with pytest.raises(ValueError):
+        codec.decode_share_vec(bad, torch.tensor([0, bad.numel()], dtype=torch.int64, device=dev()), 1)
+
+
+def test_byte_api_fixture_through_vector_codec():
+    """f3 edge cases: each case's shares, re-encoded from one-element vectors, equal the reference bytes."""
+    f3 = load_json("f3_edge.json")
+    for case in f3["cases"][:60]:
+        ys = [int.from_bytes(bytes.fromhex(s)[1 + bytes.fromhex(s)[0]:], "big") for s in case["shares"]]
+        vec = torch.from_numpy(field.ints_to_vec(ys)).to(dev())
+        for x in (1, len(ys)):
+            packed, offs = codec.encode_share_vec(vec, len(ys), x)
+            recs = codec.records_to_list(packed.cpu(), offs.cpu())
+            assert recs[x - 1] == bytes.fromhex(case["shares"][x - 1])

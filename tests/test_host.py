@@ -33,14 +33,15 @@ def header_symbols():
 
 
 def test_library_exports_header_symbols():
+    from delta_node.crypto.shamir import codec
     from delta_node.utils import _mask_native
 
     syms = header_symbols()
-    assert len(syms) >= 13
+    assert len(syms) >= 17
     L = _native.lib()
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
-    assert sorted(_native.EXPORTS + _mask_native.EXPORTS) == syms
+    assert sorted(_native.EXPORTS + _mask_native.EXPORTS + codec.EXPORTS) == syms
 
 
 def test_version_and_sizes():
