@@ -8,7 +8,7 @@ from ..crypto.shamir import _native
 
 MAX_GENS = 8
 EXPORTS = ("dn_pcg64_seed", "dn_pcg64_advance", "dn_bounded_i64_accumulate", "dn_bounded_i64_rejects",
-           "dn_unfix_precision")
+           "dn_unfix_precision", "dn_i64_sum")
 
 
 class PCG64(ctypes.Structure):
@@ -44,6 +44,8 @@ def lib() -> ctypes.CDLL:
                                                 u64, u64, vp, vp]
         L.dn_bounded_i64_rejects.restype = i32
         L.dn_bounded_i64_rejects.argtypes = [ctypes.POINTER(PCG64), u64, u64, u64, vp, vp, ctypes.c_uint32, vp]
+        L.dn_i64_sum.restype = i32
+        L.dn_i64_sum.argtypes = [ctypes.POINTER(vp), i32, vp, u64, vp]
         L.dn_unfix_precision.restype = i32
         L.dn_unfix_precision.argtypes = [vp, vp, u64, i32, vp]
         _bound = True
@@ -108,6 +110,11 @@ def list_rejects(g: PCG64, rng: int, raw_begin: int, raw_end: int, capacity: int
                                                cnt.data_ptr(), capacity, _native.stream_ptr()))
     c = int(cnt.item())
     return c, sorted(int(v) for v in idx[: min(c, capacity)].cpu().tolist())
+
+
+def i64_sum(inputs, out, n: int) -> None:
+    ptrs = (ctypes.c_void_p * len(inputs))(*[t.data_ptr() for t in inputs])
+    _native.check(lib().dn_i64_sum(ptrs, len(inputs), out.data_ptr(), n, _native.stream_ptr()))
 
 
 def unfix(inp, out, n: int, precision: int) -> None:

@@ -78,6 +78,12 @@ int dn_bounded_i64_accumulate(const dn_pcg64_t* gens, const int32_t* signs, cons
 int dn_bounded_i64_rejects(const dn_pcg64_t* gen, uint64_t rng, uint64_t raw_begin, uint64_t raw_end,
                            uint64_t* out_idx, uint32_t* count, uint32_t capacity, void* stream);
 
+/* Masked-result sum over members (reference
+ * coord/horizontal/agg.py:227-251 make_masked_results: result += val):
+ * out[e] = sum_j inputs[j][e], int64 modulo 2^64.  1 <= k <= 16 device
+ * pointers (16-byte aligned); out may alias inputs[0]. */
+int dn_i64_sum(const int64_t* const* inputs, int k, int64_t* out, uint64_t n, void* stream);
+
 /* unfix_precision: out[e] = (double)in[e] / 10^precision (precision.py:12-15). */
 int dn_unfix_precision(const int64_t* in, double* out, uint64_t n, int precision, void* stream);
 

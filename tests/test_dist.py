@@ -80,3 +80,41 @@ def test_shard_ranges_cover_exactly():
             for (a, b), (c, d) in zip(ranges, ranges[1:]):
                 assert b == c and (a % field.TILE == 0 or a == N)
             assert all(hi - lo <= sdist.shard_tiles(N, world) * field.TILE for lo, hi in ranges)
+
+
+def _allreduce_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "delta-node_amd"))
+    from delta_node.utils.agg import allreduce_sum
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(rank)
+        part = torch.from_numpy(rng.integers(-2**63, 2**63 - 1, 1000, dtype=np.int64, endpoint=True))
+        mine = part.clone()
+        allreduce_sum(part)
+        parts = [torch.from_numpy(np.random.default_rng(r).integers(-2**63, 2**63 - 1, 1000, dtype=np.int64,
+                                                                    endpoint=True)) for r in range(world)]
+        want = parts[0].clone()
+        for p in parts[1:]:
+            want += p  # int64 wrap, as numpy's += in make_masked_results
+        if rank == 0:
+            q.put(bool(torch.equal(part, want)) and not torch.equal(mine, want))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_masked_partial_sums_wrap_like_numpy():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_allreduce_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=10) is True
