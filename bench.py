@@ -101,12 +101,75 @@ def rows_bench(dev, log2n: int) -> dict:
     for sd, sg in terms:
         acc = acc + sg * pm.make_mask_numpy(sd, vs.shape)
     cpu_dt = time.perf_counter() - t0
-    return {"mask_masking": {
+    rows = {}
+    # share wire codec: encode / decode share x=3 of a 2^log2n vector (reference _share_to_bytes records)
+    from delta_node.crypto.shamir import codec, field as _field
+
+    ss = __import__("delta_node.crypto.shamir", fromlist=["SecretShare"]).SecretShare(3)
+    ss.random.seed(5)
+    blk = ss.make_shares_vec(torch.from_numpy(secrets_int64(3, n)), 5)
+    packed, offs = codec.encode_share_vec(blk[2], n, 3)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        packed, offs = codec.encode_share_vec(blk[2], n, 3, trim=False)
+    e.record()
+    torch.cuda.synchronize()
+    enc_ms = s.elapsed_time(e) / reps
+    total = int(offs[n].item())
+    s.record()
+    for _ in range(reps):
+        vec, _xs = codec.decode_share_vec(packed, offs, n)
+    e.record()
+    torch.cuda.synchronize()
+    dec_ms = s.elapsed_time(e) / reps
+    rows["share_codec"] = {"workload": f"share x=3 of 2^{log2n} elements <-> packed _share_to_bytes records",
+                           "encode_ms": enc_ms, "decode_ms": dec_ms, "bytes_out": total,
+                           "encode_elems_per_s": n / (enc_ms * 1e-3), "decode_elems_per_s": n / (dec_ms * 1e-3),
+                           "roundtrip_equal": bool(torch.equal(vec, blk[2]))}
+    # coordinator member sum: 10 int64 members
+    from delta_node.utils import sum_int64
+
+    mem = [torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device=dev) for _ in range(10)]
+    outs = torch.empty(n, dtype=torch.int64, device=dev)
+    sum_int64(mem, out=outs)
+    s.record()
+    for _ in range(reps):
+        sum_int64(mem, out=outs)
+    e.record()
+    torch.cuda.synchronize()
+    sm = s.elapsed_time(e) / reps
+    rows["member_sum"] = {"workload": f"10 members x 2^{log2n} int64 masked results", "ms": sm,
+                          "hbm_GBps": 11 * 8 * n / (sm * 1e-3) / 1e9,
+                          "equal_torch_sum": bool(torch.equal(outs, torch.stack(mem).sum(0)))}
+    # MiMC7 data commitment (utils/mimc7.py:63-92): 2^15 rows x (9 features + label), 256 Merkle roots
+    from delta_node.utils import mimc7
+    from oracle import py_mimc7
+
+    drng = np.random.default_rng(11)
+    data = drng.standard_normal((1 << 15, 10))
+    data[:, -1] = drng.integers(0, 2, 1 << 15)
+    ddev = torch.from_numpy(data).to(dev)
+    roots = mimc7.calc_data_commitment(ddev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        roots = mimc7.calc_data_commitment(ddev)
+    mm = (time.perf_counter() - t0) / 3 * 1e3
+    t0 = time.perf_counter()
+    want = py_mimc7.data_commitment(data[:256])
+    cdt = time.perf_counter() - t0
+    rows["mimc7_commitment"] = {"workload": "calc_data_commitment, 2^15 rows x 10 cols -> 256 roots",
+                                "ms": mm, "rows_per_s": (1 << 15) / (mm * 1e-3),
+                                "oracle_prefix_equal": roots[:2] == want, "bound": "valu (BN254 Montgomery mul)",
+                                "cpu_python": {"rows_per_s": 256 / cdt, "sample": "256 rows, Python ints 1 thread"}}
+    rows["mask_masking"] = {
         "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
         "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
         "hbm_GBps": 16 * n / (ms * 1e-3) / 1e9, "bound": "valu (PCG64 128-bit LCG + Lemire per draw)",
         "numpy_prefix_equal": ok,
-        "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}}
+        "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}
+    return rows
 
 
 def load_traffic(path: str):

@@ -1,0 +1,479 @@
+// mimc7_bn254.hip — MiMC7 data / weight commitments on gfx950.
+//
+// Reference: delta_node/utils/mimc7.py:18-92 over the BN254 scalar field
+// q = 0x30644e72e131a029b85045b68181585d2833e84879b9709143e1f593f0000001
+// (utils/constant.py:6-7) with 13 round constants (constant.py:14-30):
+//   mimc7_hash(x, k)      = r_13 + k,  r_0 = x,  r_{i+1} = ((r_i + k + c_i) mod q)^7 mod q
+//   mimc7_hash_arr(xs, k) = fold r <- (r + x + mimc7_hash(x, r)) mod q, r_0 = k
+//   _float2mpz(v, p)      = min(a, q - a),  a = int(v * 10^p)
+//   data commitment: rows -> field ints (features 10^8, label 10^21), zero
+//   rows padded to a multiple of 128, hash_arr(row, 2) per row, then a
+//   binary Merkle tree of hash_arr([left, right], 2) per 128-row block.
+//
+// Arithmetic: Montgomery (R = 2^256, CIOS, 8 x 32-bit limbs, one element per
+// lane); everything stays in Montgomery form between rounds (sums commute
+// with the form).  t^7 = ((t^2 t)^2) t: 4 products per round.  The row pass
+// is one lane per row (rows are independent chains); the Merkle pass is one
+// 64-lane workgroup per 128-leaf block, levels handed over through LDS.
+// The weight commitment is one sequential chain by definition (each step
+// keys the next hash): one lane, latency-bound.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "dn_internal.hpp"
+#include "dn_mimc7.h"
+
+namespace dn {
+namespace mimc {
+
+constexpr int L = 8;
+constexpr int kRounds = 13;
+
+struct Consts {
+  uint32_t q[L];
+  uint32_t qinv;          // -q^{-1} mod 2^32
+  uint32_t r2[L];         // R^2 mod q
+  uint32_t one[L];        // R mod q (1 in Montgomery form)
+  uint32_t half_q[L];     // floor(q / 2)
+  uint32_t cts[kRounds][L];  // round constants, Montgomery form
+};
+
+// ---- 256-bit helpers (host + device) ----
+__host__ __device__ inline bool geq(const uint32_t a[L], const uint32_t b[L]) {
+  for (int i = L - 1; i >= 0; --i) {
+    if (a[i] != b[i]) return a[i] > b[i];
+  }
+  return true;
+}
+
+__host__ __device__ inline uint32_t sub_in(uint32_t a[L], const uint32_t b[L]) {  // a -= b, returns borrow
+  uint64_t br = 0;
+  for (int i = 0; i < L; ++i) {
+    const uint64_t d = static_cast<uint64_t>(a[i]) - b[i] - br;
+    a[i] = static_cast<uint32_t>(d);
+    br = (d >> 63) & 1u;
+  }
+  return static_cast<uint32_t>(br);
+}
+
+__host__ __device__ inline uint32_t add_in(uint32_t a[L], const uint32_t b[L]) {  // a += b, returns carry
+  uint64_t c = 0;
+  for (int i = 0; i < L; ++i) {
+    c += static_cast<uint64_t>(a[i]) + b[i];
+    a[i] = static_cast<uint32_t>(c);
+    c >>= 32;
+  }
+  return static_cast<uint32_t>(c);
+}
+
+// a = (a + b) mod q for a, b < q (q < 2^254 so a + b < 2^255: no carry out).
+__host__ __device__ inline void addmod(uint32_t a[L], const uint32_t b[L], const uint32_t q[L]) {
+  add_in(a, b);
+  if (geq(a, q)) sub_in(a, q);
+}
+
+// CIOS Montgomery product: r = a b R^{-1} mod q (inputs < q, output < q).
+__host__ __device__ inline void mont_mul(uint32_t r[L], const uint32_t a[L], const uint32_t b[L], const Consts& k) {
+  uint32_t t[L + 2];
+  for (int i = 0; i < L + 2; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint64_t s = static_cast<uint64_t>(a[j]) * b[i] + t[j] + c;
+      t[j] = static_cast<uint32_t>(s);
+      c = s >> 32;
+    }
+    uint64_t s = static_cast<uint64_t>(t[L]) + c;
+    t[L] = static_cast<uint32_t>(s);
+    t[L + 1] = static_cast<uint32_t>(s >> 32);
+    const uint32_t m = t[0] * k.qinv;
+    c = (static_cast<uint64_t>(m) * k.q[0] + t[0]) >> 32;
+#pragma unroll
+    for (int j = 1; j < L; ++j) {
+      const uint64_t s2 = static_cast<uint64_t>(m) * k.q[j] + t[j] + c;
+      t[j - 1] = static_cast<uint32_t>(s2);
+      c = s2 >> 32;
+    }
+    s = static_cast<uint64_t>(t[L]) + c;
+    t[L - 1] = static_cast<uint32_t>(s);
+    t[L] = t[L + 1] + static_cast<uint32_t>(s >> 32);
+  }
+  for (int i = 0; i < L; ++i) r[i] = t[i];
+  if (t[L] || geq(r, k.q)) sub_in(r, k.q);
+}
+
+__host__ __device__ inline void to_mont(uint32_t r[L], const uint32_t a[L], const Consts& k) { mont_mul(r, a, k.r2, k); }
+
+__host__ __device__ inline void from_mont(uint32_t r[L], const uint32_t a[L], const Consts& k) {
+  uint32_t one[L] = {1, 0, 0, 0, 0, 0, 0, 0};
+  mont_mul(r, a, one, k);
+}
+
+// mimc7_hash in Montgomery form: (r_13 + k) mod q in `out` (Montgomery).
+__host__ __device__ inline void hash_m(uint32_t out[L], const uint32_t x[L], const uint32_t key[L], const Consts& k) {
+  uint32_t r[L];
+  for (int i = 0; i < L; ++i) r[i] = x[i];
+  for (int c = 0; c < kRounds; ++c) {
+    uint32_t t[L];
+    for (int i = 0; i < L; ++i) t[i] = r[i];
+    addmod(t, key, k.q);
+    addmod(t, k.cts[c], k.q);
+    uint32_t t2[L], t3[L], t6[L];
+    mont_mul(t2, t, t, k);
+    mont_mul(t3, t2, t, k);
+    mont_mul(t6, t3, t3, k);
+    mont_mul(r, t6, t, k);
+  }
+  for (int i = 0; i < L; ++i) out[i] = r[i];
+  addmod(out, key, k.q);
+}
+
+// One chain step of mimc7_hash_arr: r <- (r + x + mimc7_hash(x, r)) mod q.
+__host__ __device__ inline void arr_step(uint32_t r[L], const uint32_t x[L], const Consts& k) {
+  uint32_t h[L];
+  hash_m(h, x, r, k);
+  addmod(r, x, k.q);
+  addmod(r, h, k.q);
+}
+
+// _float2mpz: field value (plain, < q) of min(a, q - a), a = int(v * 10^p);
+// returns false if |v * 10^p| >= 2^253 (not handled on the device).
+__device__ inline bool float_to_field(double v, double scale, uint32_t out[L], const Consts& k) {
+  const double y = v * scale;  // the reference's float multiply
+  for (int i = 0; i < L; ++i) out[i] = 0;
+  if (y != y) return false;
+  const double ay = y < 0 ? -y : y;
+  if (!(ay < 14474011154664524427946373126085988481658748083205070504932198000989141204992.0))  // 2^253
+    return false;
+  // exact integer part of |y| as 8 limbs: mantissa * 2^e
+  int e;
+  const double m = frexp(ay, &e);  // ay = m 2^e, m in [0.5, 1)
+  if (e <= 0) return true;         // |a| = 0
+  uint64_t mant = static_cast<uint64_t>(ldexp(m, 53));  // 53-bit integer, ay = mant 2^(e-53)
+  int sh = e - 53;
+  if (sh < 0) {
+    mant >>= -sh;  // truncation toward zero (int())
+    sh = 0;
+  }
+  const int limb = sh / 32, bit = sh % 32;
+  const unsigned __int128 wide = static_cast<unsigned __int128>(mant) << bit;  // < 2^117
+  for (int i = 0; i < 4 && limb + i < L; ++i) out[limb + i] = static_cast<uint32_t>(wide >> (32 * i));
+  const bool neg = y < 0;
+  // a = +-out.  min(a, q - a): negative a -> a (value q - |a|); a > q/2 -> q - a.
+  if (neg) {
+    bool zero = true;
+    for (int i = 0; i < L; ++i) zero &= out[i] == 0;
+    if (!zero) {
+      uint32_t t[L];
+      for (int i = 0; i < L; ++i) t[i] = k.q[i];
+      sub_in(t, out);
+      for (int i = 0; i < L; ++i) out[i] = t[i];
+    }
+  } else if (!geq(k.half_q, out)) {  // a > floor(q/2)  <=>  a > q - a
+    uint32_t t[L];
+    for (int i = 0; i < L; ++i) t[i] = k.q[i];
+    sub_in(t, out);
+    for (int i = 0; i < L; ++i) out[i] = t[i];
+  }
+  return true;
+}
+
+struct RowArgs {
+  Consts k;
+  const double* data;  // [rows][cols], row-major
+  uint64_t rows, rows_pad;
+  int32_t cols;
+  double scale_feat, scale_label;
+  uint32_t* out;  // [rows_pad][8] plain canonical hashes
+  uint32_t* bad;
+};
+
+__global__ void __launch_bounds__(256) rows_kernel(const RowArgs a) {
+  const uint64_t row = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (row >= a.rows_pad) return;
+  uint32_t r[L];
+  {  // key 2 in Montgomery form
+    uint32_t two[L] = {2, 0, 0, 0, 0, 0, 0, 0};
+    to_mont(r, two, a.k);
+  }
+  bool ok = true;
+  for (int c = 0; c < a.cols; ++c) {
+    uint32_t x[L], xm[L];
+    if (row < a.rows) {
+      const double v = a.data[row * a.cols + c];
+      ok &= float_to_field(v, c == a.cols - 1 ? a.scale_label : a.scale_feat, x, a.k);
+    } else {
+      for (int i = 0; i < L; ++i) x[i] = 0;  // padding rows: [0] * cols
+    }
+    to_mont(xm, x, a.k);
+    arr_step(r, xm, a.k);
+  }
+  uint32_t h[L];
+  from_mont(h, r, a.k);
+  for (int i = 0; i < L; ++i) a.out[row * L + i] = h[i];
+  if (!ok) atomicAdd(a.bad, 1u);
+}
+
+struct MerkleArgs {
+  Consts k;
+  const uint32_t* leaves;  // [blocks * 128][8] plain
+  uint32_t* roots;         // [blocks][8] plain
+};
+
+// One workgroup of 64 lanes per 128-leaf block: level sizes 64, 32, ..., 1.
+__global__ void __launch_bounds__(64) merkle_kernel(const MerkleArgs a) {
+  __shared__ uint32_t s[64][L];
+  const uint32_t t = threadIdx.x;
+  const uint32_t* lv = a.leaves + static_cast<uint64_t>(blockIdx.x) * 128 * L;
+  uint32_t key[L];
+  {
+    uint32_t two[L] = {2, 0, 0, 0, 0, 0, 0, 0};
+    to_mont(key, two, a.k);
+  }
+  uint32_t l[L], r[L], lm[L], rm[L], acc[L];
+  for (int i = 0; i < L; ++i) {
+    l[i] = lv[(2 * t) * L + i];
+    r[i] = lv[(2 * t + 1) * L + i];
+  }
+  to_mont(lm, l, a.k);
+  to_mont(rm, r, a.k);
+  for (int i = 0; i < L; ++i) acc[i] = key[i];
+  arr_step(acc, lm, a.k);
+  arr_step(acc, rm, a.k);
+  for (int i = 0; i < L; ++i) s[t][i] = acc[i];  // Montgomery form from here on
+  __syncthreads();
+  for (uint32_t width = 32; width >= 1; width >>= 1) {
+    uint32_t nxt[L];
+    const bool act = t < width;
+    if (act) {
+      for (int i = 0; i < L; ++i) nxt[i] = key[i];
+      arr_step(nxt, s[2 * t], a.k);
+      arr_step(nxt, s[2 * t + 1], a.k);
+    }
+    __syncthreads();
+    if (act)
+      for (int i = 0; i < L; ++i) s[t][i] = nxt[i];
+    __syncthreads();
+  }
+  if (t == 0) {
+    uint32_t out[L];
+    from_mont(out, s[0], a.k);
+    for (int i = 0; i < L; ++i) a.roots[static_cast<uint64_t>(blockIdx.x) * L + i] = out[i];
+  }
+}
+
+struct ChainArgs {
+  Consts k;
+  const double* w;
+  uint64_t n;
+  double scale;
+  uint32_t key[L];  // plain
+  uint32_t* out;    // [8] plain
+  uint32_t* bad;
+};
+
+__global__ void chain_kernel(const ChainArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t r[L];
+  to_mont(r, a.key, a.k);
+  bool ok = true;
+  for (uint64_t i = 0; i < a.n; ++i) {
+    uint32_t x[L], xm[L];
+    ok &= float_to_field(a.w[i], a.scale, x, a.k);
+    to_mont(xm, x, a.k);
+    arr_step(r, xm, a.k);
+  }
+  uint32_t h[L];
+  from_mont(h, r, a.k);
+  for (int i = 0; i < L; ++i) a.out[i] = h[i];
+  if (!ok) atomicAdd(a.bad, 1u);
+}
+
+struct HashArgs {
+  Consts k;
+  const uint32_t* x;    // [n][8] plain, < q
+  const uint32_t* key;  // [n][8] plain, < q
+  uint32_t* out;        // [n][9] plain unreduced r + k (< 2q < 2^255; 9th limb 0)
+  uint64_t n;
+};
+
+__global__ void __launch_bounds__(256) hash_kernel(const HashArgs a) {
+  const uint64_t e = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= a.n) return;
+  uint32_t x[L], k[L], xm[L], km[L];
+  for (int i = 0; i < L; ++i) {
+    x[i] = a.x[e * L + i];
+    k[i] = a.key[e * L + i];
+  }
+  to_mont(xm, x, a.k);
+  to_mont(km, k, a.k);
+  uint32_t r[L];
+  for (int i = 0; i < L; ++i) r[i] = xm[i];
+  for (int c = 0; c < kRounds; ++c) {
+    uint32_t t[L];
+    for (int i = 0; i < L; ++i) t[i] = r[i];
+    addmod(t, km, a.k.q);
+    addmod(t, a.k.cts[c], a.k.q);
+    uint32_t t2[L], t3[L], t6[L];
+    mont_mul(t2, t, t, a.k);
+    mont_mul(t3, t2, t, a.k);
+    mont_mul(t6, t3, t3, a.k);
+    mont_mul(r, t6, t, a.k);
+  }
+  uint32_t rp[L];
+  from_mont(rp, r, a.k);
+  const uint32_t carry = add_in(rp, k);  // r + k, unreduced (mimc7.py:26)
+  for (int i = 0; i < L; ++i) a.out[e * 9 + i] = rp[i];
+  a.out[e * 9 + 8] = carry;
+}
+
+// ---- host: constants ----
+void make_consts(Consts& k) {
+  static const uint32_t q[L] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  std::memcpy(k.q, q, sizeof(q));
+  // qinv = -q^{-1} mod 2^32 (Newton)
+  uint32_t inv = q[0];
+  for (int i = 0; i < 5; ++i) inv *= 2u - q[0] * inv;
+  k.qinv = 0u - inv;
+  // R mod q and R^2 mod q by doubling 1 (mod q) 256 / 512 times
+  uint32_t v[L] = {1, 0, 0, 0, 0, 0, 0, 0};
+  for (int it = 1; it <= 512; ++it) {
+    uint32_t t[L];
+    std::memcpy(t, v, sizeof(t));
+    addmod(v, t, q);
+    if (it == 256) std::memcpy(k.one, v, sizeof(v));
+  }
+  std::memcpy(k.r2, v, sizeof(v));
+  // floor(q / 2)
+  for (int i = 0; i < L; ++i) k.half_q[i] = (q[i] >> 1) | (i + 1 < L ? (q[i + 1] << 31) : 0u);
+}
+
+}  // namespace mimc
+}  // namespace dn
+
+using namespace dn;
+using namespace dn::mimc;
+
+namespace {
+// Round constants: decimal strings of utils/constant.py:14-30 (the circomlib
+// MiMC7 constants), parsed once per call into 8 limbs and Montgomery form.
+const char* kCtsDec[kRounds] = {
+    "0",
+    "20888961410941983456478427210666206549300505294776164667214940546594746570981",
+    "15265126113435022738560151911929040668591755459209400716467504685752745317193",
+    "8334177627492981984476504167502758309043212251641796197711684499645635709656",
+    "1374324219480165500871639364801692115397519265181803854177629327624133579404",
+    "11442588683664344394633565859260176446561886575962616332903193988751292992472",
+    "2558901189096558760448896669327086721003508630712968559048179091037845349145",
+    "11189978595292752354820141775598510151189959177917284797737745690127318076389",
+    "3262966573163560839685415914157855077211340576201936620532175028036746741754",
+    "17029914891543225301403832095880481731551830725367286980611178737703889171730",
+    "4614037031668406927330683909387957156531244689520944789503628527855167665518",
+    "19647356996769918391113967168615123299113119185942498194367262335168397100658",
+    "5040699236106090655289931820723926657076483236860546282406111821875672148900"};
+
+void dec_to_limbs(const char* s, uint32_t out[L]) {
+  for (int i = 0; i < L; ++i) out[i] = 0;
+  for (; *s; ++s) {  // out = out * 10 + digit
+    uint64_t c = static_cast<uint64_t>(*s - '0');
+    for (int i = 0; i < L; ++i) {
+      const uint64_t t = static_cast<uint64_t>(out[i]) * 10u + c;
+      out[i] = static_cast<uint32_t>(t);
+      c = t >> 32;
+    }
+  }
+}
+
+void consts(Consts& k) {
+  std::memset(&k, 0, sizeof(k));
+  make_consts(k);
+  for (int c = 0; c < kRounds; ++c) {
+    uint32_t plain[L];
+    dec_to_limbs(kCtsDec[c], plain);
+    to_mont(k.cts[c], plain, k);
+  }
+}
+
+double pow10d(int p) {
+  double s = 1.0;
+  for (int i = 0; i < p; ++i) s *= 10.0;
+  return s;
+}
+}  // namespace
+
+extern "C" int dn_mimc7_data_rows(const double* data, uint64_t rows, int cols, uint32_t* row_hashes,
+                                  uint32_t* bad_count, void* stream) {
+  if (cols < 1 || rows == 0) return set_error(DN_ERR_ARG, "dn_mimc7_data_rows: empty data");
+  if (!data || !row_hashes || !bad_count) return set_error(DN_ERR_ARG, "dn_mimc7_data_rows: null pointer");
+  RowArgs a;
+  std::memset(&a, 0, sizeof(a));
+  consts(a.k);
+  a.data = data;
+  a.rows = rows;
+  a.rows_pad = (rows + 127) / 128 * 128;
+  a.cols = cols;
+  a.scale_feat = pow10d(8);
+  a.scale_label = pow10d(21);
+  a.out = row_hashes;
+  a.bad = bad_count;
+  hipLaunchKernelGGL(rows_kernel, dim3(static_cast<uint32_t>((a.rows_pad + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mimc7_data_rows: %s", hipGetErrorString(err));
+  return DN_OK;
+}
+
+extern "C" int dn_mimc7_merkle_blocks(const uint32_t* leaves, uint64_t blocks, uint32_t* roots, void* stream) {
+  if (blocks == 0) return DN_OK;
+  if (!leaves || !roots) return set_error(DN_ERR_ARG, "dn_mimc7_merkle_blocks: null pointer");
+  MerkleArgs a;
+  std::memset(&a, 0, sizeof(a));
+  consts(a.k);
+  a.leaves = leaves;
+  a.roots = roots;
+  hipLaunchKernelGGL(merkle_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(64), 0,
+                     static_cast<hipStream_t>(stream), a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mimc7_merkle_blocks: %s", hipGetErrorString(err));
+  return DN_OK;
+}
+
+extern "C" int dn_mimc7_weight_chain(const double* w, uint64_t n, int precision, uint32_t* out, uint32_t* bad_count,
+                                    void* stream) {
+  if (!w || !out || !bad_count) return set_error(DN_ERR_ARG, "dn_mimc7_weight_chain: null pointer");
+  if (precision < 0 || precision > 22) return set_error(DN_ERR_ARG, "dn_mimc7_weight_chain: precision 0..22");
+  ChainArgs a;
+  std::memset(&a, 0, sizeof(a));
+  consts(a.k);
+  a.w = w;
+  a.n = n;
+  a.scale = pow10d(precision);
+  a.key[0] = 2;
+  a.out = out;
+  a.bad = bad_count;
+  hipLaunchKernelGGL(chain_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mimc7_weight_chain: %s", hipGetErrorString(err));
+  return DN_OK;
+}
+
+extern "C" int dn_mimc7_hash(const uint32_t* xs, const uint32_t* keys, uint64_t n, uint32_t* out, void* stream) {
+  if (n == 0) return DN_OK;
+  if (!xs || !keys || !out) return set_error(DN_ERR_ARG, "dn_mimc7_hash: null pointer");
+  HashArgs a;
+  std::memset(&a, 0, sizeof(a));
+  consts(a.k);
+  a.x = xs;
+  a.key = keys;
+  a.out = out;
+  a.n = n;
+  hipLaunchKernelGGL(hash_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mimc7_hash: %s", hipGetErrorString(err));
+  return DN_OK;
+}

@@ -34,14 +34,14 @@ def header_symbols():
 
 def test_library_exports_header_symbols():
     from delta_node.crypto.shamir import codec
-    from delta_node.utils import _mask_native
+    from delta_node.utils import _mask_native, mimc7
 
     syms = header_symbols()
-    assert len(syms) >= 17
+    assert len(syms) >= 21
     L = _native.lib()
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
-    assert sorted(_native.EXPORTS + _mask_native.EXPORTS + codec.EXPORTS) == syms
+    assert sorted(_native.EXPORTS + _mask_native.EXPORTS + codec.EXPORTS + mimc7.EXPORTS) == syms
 
 
 def test_version_and_sizes():
