@@ -33,6 +33,8 @@ struct SplitArgs {
   uint64_t n_elem;
   uint64_t ntiles;
   uint64_t vec_bytes;
+  uint64_t coeff_stride;  // bytes between coefficient rows (>= vec_bytes)
+  uint64_t share_stride;  // bytes between share rows (>= vec_bytes)
   int32_t n_shares;
   int32_t threshold;  // runtime t (generic kernel only)
 };
@@ -86,7 +88,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
       load_secret<FE_SECRET>(a, tile, w, c[0]);
 #pragma unroll
       for (int j = 1; j < T; ++j)
-        load_fe_b(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.vec_bytes, tile)), w, c[j]);
+        load_fe_b(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.coeff_stride, tile)), w, c[j]);
       if constexpr (!FOLD) {
         // In place, c becomes the forward-difference table at x = 1:
         // synthetic division by (x - z) for z = 1..T-1 turns the monomial
@@ -130,7 +132,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
         uint32_t (&D)[T][kLimbs] = c;
 #pragma unroll 1
         for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
-          store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile)), w, D[0]);
+          store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), w, D[0]);
           fd_step<T>(D);
         }
       } else {
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
             }
           }
           reduce(v);
-          store_fe_b(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile)), w, v);
+          store_fe_b(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), w, v);
         }
       }
     }
@@ -177,17 +179,17 @@ __global__ void __launch_bounds__(kBlock) split_kernel_generic(const SplitArgs a
       for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
         const uint32_t x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(xi));
         uint32_t v[kLimbs];
-        load_fe_cached(tile_base(a.coeffs + static_cast<uint64_t>(a.threshold - 2) * a.vec_bytes, tile), w, v);
+        load_fe_cached(tile_base(a.coeffs + static_cast<uint64_t>(a.threshold - 2) * a.coeff_stride, tile), w, v);
 #pragma unroll 1
         for (int j = a.threshold - 3; j >= 0; --j) {
           uint32_t cj[kLimbs];
-          load_fe_cached(tile_base(a.coeffs + static_cast<uint64_t>(j) * a.vec_bytes, tile), w, cj);
+          load_fe_cached(tile_base(a.coeffs + static_cast<uint64_t>(j) * a.coeff_stride, tile), w, cj);
           mul_small_add(v, x, cj);
           fold(v);
         }
         mul_small_add(v, x, c0);
         reduce(v);
-        store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vec_bytes, tile), w, v);
+        store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile), w, v);
       }
     }
   }
@@ -368,6 +370,12 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
     return set_error(DN_ERR_ARG, "%s: null pointer", name);
   a.ntiles = (a.n_elem + kTile - 1) / kTile;
   a.vec_bytes = a.ntiles * kTileBytes;
+  {  // DN_ROW_PAD: experimental row pitch = vec_bytes + pad (placement probe only)
+    const char* rp = std::getenv("DN_ROW_PAD");
+    const uint64_t pad = rp ? std::strtoull(rp, nullptr, 10) : 0;
+    a.coeff_stride = a.vec_bytes + pad;
+    a.share_stride = a.vec_bytes + pad;
+  }
   a.n_shares = n_shares;
   a.threshold = threshold;
   const dim3 g(grid_for(a.ntiles));
