@@ -35,12 +35,25 @@ struct SplitArgs {
   uint64_t vec_bytes;
   uint64_t coeff_stride;  // bytes between coefficient rows (>= vec_bytes)
   uint64_t share_stride;  // bytes between share rows (>= vec_bytes)
+  uint32_t xcd_chunk;     // 1: XCD-contiguous wave numbering (grid % 8 == 0)
   int32_t n_shares;
   int32_t threshold;  // runtime t (generic kernel only)
 };
 
 constexpr int kBlock = 256;  // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
+constexpr uint32_t kXcds = 8;
+
+// First tile of this wave.  Workgroups are dispatched to the 8 XCDs round-
+// robin (XCD = blockIdx % 8); with xcd_chunk the grid is renumbered so that
+// XCD x works the x-th contiguous eighth of each grid-stride pass, i.e. the
+// workgroups resident on one XCD touch adjacent tiles (a footprint 8x smaller
+// per XCD L2 / translation cache) instead of every 8th block of the window.
+__device__ __forceinline__ uint32_t first_wave(uint32_t xcd_chunk) {
+  uint32_t b = blockIdx.x;
+  if (xcd_chunk) b = (b % kXcds) * (gridDim.x / kXcds) + b / kXcds;
+  return b * kWavesPerBlock + (threadIdx.x >> 6);
+}
 
 template <bool FE_SECRET>
 __device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, uint32_t w, uint32_t c0[kLimbs]) {
@@ -77,7 +90,7 @@ template <int T, bool FE_SECRET, bool FOLD>
 __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
   for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
 #pragma unroll 1
     for (uint32_t q = 0; q < 4; ++q) {
@@ -166,7 +179,7 @@ template <bool FE_SECRET>
 __global__ void __launch_bounds__(kBlock) split_kernel_generic(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
   for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
 #pragma unroll 1
     for (uint32_t q = 0; q < 4; ++q) {
@@ -202,6 +215,7 @@ struct ReconArgs {
   uint32_t* overflow;
   uint64_t n_elem;
   uint64_t ntiles;
+  uint32_t xcd_chunk;
   int32_t k;
   uint32_t neg;
   uint32_t shift;
@@ -226,7 +240,7 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
   constexpr int VB = (A == kLimbs) ? 1046 : (521 + 32 * A + 4);
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
   for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
 #pragma unroll 1
     for (uint32_t q = 0; q < 4; ++q) {
@@ -326,6 +340,12 @@ static int grid_for(uint64_t ntiles) {
   return static_cast<int>(blocks < cap ? blocks : cap);
 }
 
+// DN_TILE_MAP=1 selects the XCD-contiguous numbering (A/B hook, read per call).
+static uint32_t xcd_chunk_for(int grid) {
+  const char* s = std::getenv("DN_TILE_MAP");
+  return (s && s[0] == '1' && grid % static_cast<int>(kXcds) == 0) ? 1u : 0u;
+}
+
 static int check_launch(const char* what) {
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: launch failed: %s", what, hipGetErrorString(err));
@@ -379,6 +399,7 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   a.n_shares = n_shares;
   a.threshold = threshold;
   const dim3 g(grid_for(a.ntiles));
+  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
   hipStream_t s = static_cast<hipStream_t>(stream);
   // DN_SPLIT_HORNER=1 forces the Horner kernel (A/B hook, read per call).
   const char* hz = std::getenv("DN_SPLIT_HORNER");
@@ -442,6 +463,7 @@ extern "C" int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_
   std::memcpy(a.a, w->a, sizeof(a.a));
   std::memcpy(a.inv, w->inv, sizeof(a.inv));
   const dim3 g(grid_for(a.ntiles));
+  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
   hipStream_t s = static_cast<hipStream_t>(stream);
   a.d = w->d;
   a.d_inv32 = w->d_inv32;
