@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "chacha_device.hpp"
 #include "dn_internal.hpp"
 #include "m521_device.hpp"
 
@@ -38,6 +39,8 @@ struct SplitArgs {
   uint32_t xcd_chunk;     // 1: XCD-contiguous wave numbering (grid % 8 == 0)
   int32_t n_shares;
   int32_t threshold;  // runtime t (generic kernel only)
+  uint64_t elem_offset;  // PRNG coefficients: global index of element 0 (multiple of 256)
+  ChachaKey key;         // PRNG coefficients: key, nonce, rounds
 };
 
 constexpr int kBlock = 256;  // 4 waves
@@ -86,22 +89,70 @@ constexpr int64_t fd_factorial(int k) { return k <= 1 ? 1 : k * fd_factorial(k -
 // f(x) is reduced.
 // FOLD == true (large n or t): Horner per share (as _eval_at, shamir.py:19-25)
 // with a Mersenne fold after every step.
-template <int T, bool FE_SECRET, bool FOLD>
+//
+// PRNG == true: coefficients are not read but generated (dn_m521_split_prng,
+// chacha_device.hpp): per tile, the wave first computes the 16 (T-1) blocks
+// holding the tile's top limbs (one block per lane) into its LDS slice, then
+// each lane generates its element's T-1 low blocks in place in c[1..T-1].
+template <int T>
+__device__ __forceinline__ void prng_tile_tops(const SplitArgs& a, uint32_t tile, uint32_t lane, uint32_t* tops) {
+  constexpr uint32_t kBlocks = 16u * (T - 1);  // 256 (T-1) top words per tile
+  const uint64_t g0 = a.elem_offset + static_cast<uint64_t>(tile) * kTile;
+  const uint64_t b0 = kTopDomain + g0 * (T - 1) / 16u;
+  __builtin_amdgcn_wave_barrier();  // previous tile's reads are done
+#pragma unroll 1
+  for (uint32_t b = lane; b < kBlocks; b += 64u) {
+    uint32_t x[16];
+    chacha_block(x, a.key, b0 + b);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tops[b * 16u + i] = x[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int T>
+__device__ __forceinline__ void prng_coeffs_of(const SplitArgs& a, uint32_t tile, uint32_t w, const uint32_t* tops,
+                                               uint32_t c[T][kLimbs]) {
+  const uint64_t g = a.elem_offset + static_cast<uint64_t>(tile) * kTile + w;
+#pragma unroll
+  for (int j = 1; j < T; ++j) {
+    const uint64_t i = g * (T - 1) + (j - 1);
+    chacha_block(c[j], a.key, i);
+    c[j][16] = tops[w * (T - 1) + (j - 1)] & kTopMask;
+    if (__builtin_expect(prng_rejected(c[j]), 0)) prng_retry(c[j], a.key, i);
+    add_small(c[j], 1u);
+  }
+}
+
+constexpr int kMaxPrngT = 8;
+
+template <int T, bool FE_SECRET, bool FOLD, bool PRNG = false>
 __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
   const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
+  static_assert(!PRNG || (T >= 2 && !FE_SECRET), "PRNG coefficients: u64 secrets, t >= 2");
+  // PRNG: per-wave slice of the tile's top-limb words
+  __shared__ uint32_t s_tops[PRNG ? kWavesPerBlock : 1][PRNG ? 256 * (T - 1) : 1];
+  uint32_t* tops = s_tops[PRNG ? (threadIdx.x >> 6) : 0];
   for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+    if constexpr (PRNG) prng_tile_tops<T>(a, tile, lane, tops);
 #pragma unroll 1
     for (uint32_t q = 0; q < 4; ++q) {
       const uint32_t w = lane + 64u * q;
       const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
       if (e >= a.n_elem) break;
       uint32_t c[T][kLimbs];
-      load_secret<FE_SECRET>(a, tile, w, c[0]);
+      if constexpr (PRNG) {
+        prng_coeffs_of<T>(a, tile, w, tops, c);
+      } else {
 #pragma unroll
-      for (int j = 1; j < T; ++j)
-        load_fe_b(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.coeff_stride, tile)), w, c[j]);
+        for (int j = 1; j < T; ++j)
+          load_fe_b(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.coeff_stride, tile)), w, c[j]);
+      }
+      load_secret<FE_SECRET>(a, tile, w, c[0]);
       if constexpr (!FOLD) {
         // In place, c becomes the forward-difference table at x = 1:
         // synthetic division by (x - z) for z = 1..T-1 turns the monomial
@@ -204,6 +255,31 @@ __global__ void __launch_bounds__(kBlock) split_kernel_generic(const SplitArgs a
         reduce(v);
         store_fe(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile), w, v);
       }
+    }
+  }
+}
+
+// The PRNG coefficient stream written out as the tiled block a.coeffs
+// (dn_m521_prng_coeffs): rows j-1 = coefficient j, same values split_prng uses.
+template <int T>
+__global__ void __launch_bounds__(kBlock) prng_coeffs_kernel(const SplitArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
+  __shared__ uint32_t s_tops[kWavesPerBlock][256 * (T - 1)];
+  uint32_t* tops = s_tops[threadIdx.x >> 6];
+  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+    prng_tile_tops<T>(a, tile, lane, tops);
+#pragma unroll 1
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t w = lane + 64u * q;
+      if (static_cast<uint64_t>(tile) * kTile + w >= a.n_elem) break;
+      uint32_t c[T][kLimbs];
+      prng_coeffs_of<T>(a, tile, w, tops, c);
+#pragma unroll
+      for (int j = 1; j < T; ++j)
+        store_fe_b(tile_rsrc(tile_base(const_cast<uint8_t*>(a.coeffs) + static_cast<uint64_t>(j - 1) * a.coeff_stride,
+                                       tile)), w, c[j]);
     }
   }
 }
@@ -379,14 +455,58 @@ static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
   }
 }
 
-static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, bool fe, const char* name) {
+template <bool FOLD>
+static void launch_split_prng(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
+  switch (t) {
+    case 2: hipLaunchKernelGGL((split_kernel<2, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((split_kernel<3, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((split_kernel<4, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((split_kernel<5, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((split_kernel<6, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((split_kernel<7, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((split_kernel<8, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    default: break;
+  }
+}
+
+static void launch_prng_coeffs(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
+  switch (t) {
+    case 2: hipLaunchKernelGGL((prng_coeffs_kernel<2>), g, dim3(kBlock), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((prng_coeffs_kernel<3>), g, dim3(kBlock), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((prng_coeffs_kernel<4>), g, dim3(kBlock), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((prng_coeffs_kernel<5>), g, dim3(kBlock), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((prng_coeffs_kernel<6>), g, dim3(kBlock), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((prng_coeffs_kernel<7>), g, dim3(kBlock), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((prng_coeffs_kernel<8>), g, dim3(kBlock), 0, s, a); break;
+    default: break;
+  }
+}
+
+static int set_prng_key(SplitArgs& a, const uint32_t* key, uint64_t nonce, int rounds, uint64_t elem_offset,
+                        const char* name) {
+  if (!key) return set_error(DN_ERR_ARG, "%s: null key", name);
+  if (!(rounds == 8 || rounds == 12 || rounds == 20))
+    return set_error(DN_ERR_ARG, "%s: rounds must be 8, 12 or 20 (got %d)", name, rounds);
+  if (elem_offset % kTile) return set_error(DN_ERR_ARG, "%s: elem_offset must be a multiple of %d", name, kTile);
+  std::memcpy(a.key.k, key, sizeof(a.key.k));
+  a.key.n0 = static_cast<uint32_t>(nonce);
+  a.key.n1 = static_cast<uint32_t>(nonce >> 32);
+  a.key.rounds = rounds;
+  a.elem_offset = elem_offset;
+  return DN_OK;
+}
+
+static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, bool fe, const char* name,
+                        bool prng = false) {
   if (threshold < 1 || threshold > DN_MAX_THRESHOLD)
     return set_error(DN_ERR_UNSUPPORTED, "%s: threshold %d outside 1..%d", name, threshold, DN_MAX_THRESHOLD);
   if (threshold > n_shares) return set_error(DN_ERR_THRESHOLD, "threshold should be little equal than shares");
   if (n_shares > DN_MAX_SHARES)
     return set_error(DN_ERR_UNSUPPORTED, "%s: %d shares > %d", name, n_shares, DN_MAX_SHARES);
   if (a.n_elem == 0) return DN_OK;
-  if (!a.shares || (threshold > 1 && !a.coeffs) || (fe ? !a.sec_fe : !a.sec_u64))
+  if (prng && threshold > kMaxPrngT)
+    return set_error(DN_ERR_UNSUPPORTED, "%s: threshold %d > %d", name, threshold, kMaxPrngT);
+  if (!a.shares || (threshold > 1 && !prng && !a.coeffs) || (fe ? !a.sec_fe : !a.sec_u64))
     return set_error(DN_ERR_ARG, "%s: null pointer", name);
   a.ntiles = (a.n_elem + kTile - 1) / kTile;
   a.vec_bytes = a.ntiles * kTileBytes;
@@ -404,7 +524,10 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   // DN_SPLIT_HORNER=1 forces the Horner kernel (A/B hook, read per call).
   const char* hz = std::getenv("DN_SPLIT_HORNER");
   const bool fold_each = needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
-  if (fe) {
+  if (prng && threshold > 1) {
+    if (fold_each) launch_split_prng<true>(threshold, g, s, a);
+    else launch_split_prng<false>(threshold, g, s, a);
+  } else if (fe) {
     if (fold_each) launch_split_t<true, true>(threshold, g, s, a);
     else launch_split_t<true, false>(threshold, g, s, a);
   } else {
@@ -426,6 +549,38 @@ extern "C" int dn_m521_split_u64(const int64_t* secrets, const void* coeffs, voi
   a.shares = static_cast<uint8_t*>(shares);
   a.n_elem = n_elem;
   return split_common(a, threshold, n_shares, stream, false, "dn_m521_split_u64");
+}
+
+extern "C" int dn_m521_split_prng(const int64_t* secrets, const uint32_t* key, uint64_t nonce, int rounds,
+                                  uint64_t elem_offset, void* shares, uint64_t n_elem, int threshold, int n_shares,
+                                  void* stream) {
+  SplitArgs a{};
+  const int rc = set_prng_key(a, key, nonce, rounds, elem_offset, "dn_m521_split_prng");
+  if (rc != DN_OK) return rc;
+  a.sec_u64 = secrets;
+  a.shares = static_cast<uint8_t*>(shares);
+  a.n_elem = n_elem;
+  return split_common(a, threshold, n_shares, stream, false, "dn_m521_split_prng", true);
+}
+
+extern "C" int dn_m521_prng_coeffs(const uint32_t* key, uint64_t nonce, int rounds, uint64_t elem_offset,
+                                   void* coeffs, uint64_t n_elem, int tm1, void* stream) {
+  SplitArgs a{};
+  const int rc = set_prng_key(a, key, nonce, rounds, elem_offset, "dn_m521_prng_coeffs");
+  if (rc != DN_OK) return rc;
+  if (tm1 < 1 || tm1 + 1 > kMaxPrngT)
+    return set_error(DN_ERR_UNSUPPORTED, "dn_m521_prng_coeffs: %d coefficients outside 1..%d", tm1, kMaxPrngT - 1);
+  if (n_elem == 0) return DN_OK;
+  if (!coeffs) return set_error(DN_ERR_ARG, "dn_m521_prng_coeffs: null pointer");
+  a.coeffs = static_cast<const uint8_t*>(coeffs);
+  a.n_elem = n_elem;
+  a.ntiles = (n_elem + kTile - 1) / kTile;
+  a.vec_bytes = a.ntiles * kTileBytes;
+  a.coeff_stride = a.vec_bytes;
+  const dim3 g(grid_for(a.ntiles));
+  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
+  launch_prng_coeffs(tm1 + 1, g, static_cast<hipStream_t>(stream), a);
+  return check_launch("dn_m521_prng_coeffs");
 }
 
 extern "C" int dn_m521_split_fe(const void* secrets_fe, const void* coeffs, void* shares, uint64_t n_elem,

@@ -37,6 +37,7 @@ DEFAULT_LIB = os.path.normpath(os.path.join(_HERE, "..", "..", "..", "lib", "lib
 EXPORTS = (
     "dn_m521_vec_bytes", "dn_m521_split_u64", "dn_m521_split_fe", "dn_m521_lagrange",
     "dn_m521_reconstruct", "dn_mt19937_draw_coeffs", "dn_last_error", "dn_version",
+    "dn_m521_split_prng", "dn_m521_prng_coeffs",
 )
 
 
@@ -92,6 +93,10 @@ def lib() -> ctypes.CDLL:
         L.dn_m521_split_fe.restype = i32
         L.dn_m521_split_fe.argtypes = [vp, vp, vp, u64, i32, i32, vp]
         L.dn_m521_lagrange.restype = i32
+        L.dn_m521_split_prng.restype = i32
+        L.dn_m521_split_prng.argtypes = [vp, vp, u64, i32, u64, vp, u64, i32, i32, vp]
+        L.dn_m521_prng_coeffs.restype = i32
+        L.dn_m521_prng_coeffs.argtypes = [vp, u64, i32, u64, vp, u64, i32, vp]
         L.dn_m521_lagrange.argtypes = [ctypes.POINTER(ctypes.c_uint64), i32, i32, ctypes.POINTER(Lagrange)]
         L.dn_m521_reconstruct.restype = i32
         L.dn_m521_reconstruct.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(Lagrange), vp, vp, vp, u64, vp]
@@ -154,6 +159,22 @@ def split_u64(secrets, coeffs, shares, n: int, t: int, n_shares: int) -> None:
 
 def split_fe(secrets_fe, coeffs, shares, n: int, t: int, n_shares: int) -> None:
     check(lib().dn_m521_split_fe(_ptr(secrets_fe), _ptr(coeffs), _ptr(shares), n, t, n_shares, stream_ptr()))
+
+
+def _key_words(key: bytes):
+    if not isinstance(key, (bytes, bytearray)) or len(key) != 32:
+        raise ValueError("PRNG key must be 32 bytes")
+    return (ctypes.c_uint32 * 8).from_buffer_copy(bytes(key))
+
+
+def split_prng(secrets, key: bytes, nonce: int, rounds: int, elem_offset: int, shares, n: int, t: int,
+               n_shares: int) -> None:
+    check(lib().dn_m521_split_prng(_ptr(secrets), _key_words(key), nonce, rounds, elem_offset, _ptr(shares), n, t,
+                                   n_shares, stream_ptr()))
+
+
+def prng_coeffs(key: bytes, nonce: int, rounds: int, elem_offset: int, coeffs, n: int, tm1: int) -> None:
+    check(lib().dn_m521_prng_coeffs(_key_words(key), nonce, rounds, elem_offset, _ptr(coeffs), n, tm1, stream_ptr()))
 
 
 def lagrange(xs: Sequence[int], threshold: int) -> Lagrange:

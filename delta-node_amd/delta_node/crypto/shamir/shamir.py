@@ -240,6 +240,45 @@ class SecretShare(object):
             _native.split_u64(vals, coeffs if t > 1 else None, out, n, t, shares)
         return out
 
+    def make_shares_vec_prng(self, values, shares: int, *, key: Optional[bytes] = None, nonce: int = 0,
+                             rounds: int = 20, elem_offset: int = 0, out=None):
+        """Split every element with coefficients generated on the device.
+
+        Same shares layout as `make_shares_vec`, but the coefficients come from
+        a keyed ChaCha stream (dn_m521_split_prng) instead of `self.random`:
+        each is uniform in [1, p-1] and depends only on (key, nonce, global
+        element index elem_offset + e), so sharded calls reproduce the
+        unsharded result.  key: 32 bytes (default: fresh from `secrets`);
+        rounds: 20 (default), 12 or 8.  Returns (shares block, key).
+        """
+        import secrets as _secrets
+
+        import torch
+
+        if self.threshold > shares:
+            raise ValueError("threshold should be little equal than shares")
+        if shares > _native.MAX_SHARES or self.threshold > 8:
+            raise NotImplementedError("make_shares_vec_prng: at most 65535 shares and threshold 8")
+        if key is None:
+            key = _secrets.token_bytes(32)
+        dev = _device()
+        vals = torch.as_tensor(values)
+        if vals.dtype not in (torch.int64, torch.uint64):
+            raise TypeError("make_shares_vec_prng: values must be an int64 tensor")
+        vals = vals.reshape(-1).to(dev).contiguous()
+        n = vals.numel()
+        vb = field.vec_bytes(n)
+        if out is None:
+            out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
+        elif out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous():
+            raise ValueError(f"make_shares_vec_prng: out must be contiguous uint8 [{shares}, {vb}]")
+        if shares > 0:
+            if self.threshold <= 1:
+                _native.split_u64(vals, None, out, n, 1, shares)
+            else:
+                _native.split_prng(vals, key, nonce, rounds, elem_offset, out, n, self.threshold, shares)
+        return out, key
+
     def resolve_shares_vec(self, shares, xs: Sequence[int], n: int, *, out: str = "int64",
                            return_overflow: bool = False):
         """Interpolate share vectors at 0 (vector form of `resolve_shares`).

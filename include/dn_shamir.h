@@ -86,6 +86,28 @@ int dn_m521_split_u64(const int64_t* secrets, const void* coeffs, void* shares,
 int dn_m521_split_fe(const void* secrets_fe, const void* coeffs, void* shares,
                      uint64_t n_elem, int threshold, int n_shares, void* stream);
 
+/* Split with coefficients generated on the device (SURVEY.md §8(b)
+ * dn_m521_split_prng, §8(d) config 2'): no coefficient input, 8 + 66 n bytes
+ * of HBM traffic per element.  Replaces make_shares' coefficient source —
+ * self.random (CPython MT19937, shamir.py:59-61) — by a keyed stream cipher:
+ * coefficient j (1..t-1) of GLOBAL element g = elem_offset + e has index
+ * i = g (t-1) + j - 1; its limbs 0..15 are ChaCha block i (64-bit counter,
+ * 64-bit nonce, `rounds` in {8, 12, 20}; key = 8 host words), limb 16 is the
+ * low 9 bits of word i % 16 of block 2^62 + i / 16; a value >= p - 1 is
+ * redrawn from blocks 2^63 + (i << 6) + 2a, +1 (attempt a) — randint's
+ * reject rule — and 1 is added, so every coefficient is uniform in [1, p-1].
+ * The stream depends only on (key, nonce, g): sharded calls (elem_offset a
+ * multiple of 256) produce exactly the unsharded result.  u64 secrets,
+ * 2 <= t <= 8 (t = 1 needs no coefficients).  Restated on the CPU in
+ * oracle/chacha_oracle.c. */
+int dn_m521_split_prng(const int64_t* secrets, const uint32_t* key, uint64_t nonce, int rounds, uint64_t elem_offset,
+                       void* shares, uint64_t n_elem, int threshold, int n_shares, void* stream);
+
+/* The same coefficient stream written out as a tiled block of tm1 vectors
+ * (row j-1 = coefficient j), e.g. for dn_m521_split_fe; 1 <= tm1 <= 7. */
+int dn_m521_prng_coeffs(const uint32_t* key, uint64_t nonce, int rounds, uint64_t elem_offset, void* coeffs,
+                        uint64_t n_elem, int tm1, void* stream);
+
 /*
  * Lagrange-at-0 weights for share abscissas xs[0..k-1], in the form the
  * reconstruct kernel consumes:  lambda_i = a_i / (d * 2^shift)  (mod p), with

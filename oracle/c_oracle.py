@@ -20,7 +20,10 @@ def lib():
         L.oracle_mt_words.argtypes = [u64, u64, vp]
         L.oracle_split.argtypes = [vp, vp, u64, i32, i32, vp]
         L.oracle_reconstruct.argtypes = [vp, vp, i32, u64, vp]
-        for f in (L.oracle_draw_coeffs, L.oracle_mt_words, L.oracle_split, L.oracle_reconstruct):
+        L.oracle_chacha_block.argtypes = [vp, u64, u64, i32, vp]
+        L.oracle_prng_coeffs.argtypes = [vp, u64, i32, u64, u64, i32, vp]
+        for f in (L.oracle_draw_coeffs, L.oracle_mt_words, L.oracle_split, L.oracle_reconstruct,
+                  L.oracle_chacha_block, L.oracle_prng_coeffs):
             f.restype = None
         _lib = L
     return _lib
@@ -31,6 +34,26 @@ def draw_coeffs(seed: int, n: int, tm1: int) -> np.ndarray:
     out = np.zeros((n, tm1, 17), dtype=np.uint32)
     if n and tm1:
         lib().oracle_draw_coeffs(seed, n, tm1, out.ctypes.data)
+    return out
+
+
+def _key_words(key: bytes) -> np.ndarray:
+    assert len(key) == 32
+    return np.frombuffer(key, dtype="<u4").copy()
+
+
+def chacha_block(key: bytes, counter: int, nonce: int, rounds: int = 20) -> np.ndarray:
+    """One 16-word keystream block (64-bit counter in words 12-13, nonce in 14-15)."""
+    out = np.zeros(16, dtype=np.uint32)
+    lib().oracle_chacha_block(_key_words(key).ctypes.data, counter, nonce, rounds, out.ctypes.data)
+    return out
+
+
+def prng_coeffs(key: bytes, nonce: int, elem_offset: int, n: int, tm1: int, rounds: int = 20) -> np.ndarray:
+    """dn_m521_split_prng's coefficients of elements elem_offset..+n: uint32 [n, tm1, 17]."""
+    out = np.zeros((n, tm1, 17), dtype=np.uint32)
+    if n and tm1:
+        lib().oracle_prng_coeffs(_key_words(key).ctypes.data, nonce, rounds, elem_offset, n, tm1, out.ctypes.data)
     return out
 
 
