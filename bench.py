@@ -127,6 +127,28 @@ def rows_bench(dev, log2n: int) -> dict:
                            "encode_ms": enc_ms, "decode_ms": dec_ms, "bytes_out": total,
                            "encode_elems_per_s": n / (enc_ms * 1e-3), "decode_elems_per_s": n / (dec_ms * 1e-3),
                            "roundtrip_equal": bool(torch.equal(vec, blk[2]))}
+    # device-PRNG split (dn_m521_split_prng, SURVEY §8(d) config 2'): coefficients generated in-kernel
+    from delta_node.crypto.shamir import _native as _nat
+
+    sh = torch.empty((5, _field.vec_bytes(n)), dtype=torch.uint8, device=dev)
+    sec = torch.from_numpy(secrets_int64(3, n)).to(dev)
+    prng = {}
+    for rounds in (20, 8):
+        _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, sh, n, 3, 5)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(reps):
+            _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, sh, n, 3, 5)
+        e.record()
+        torch.cuda.synchronize()
+        pm = s.elapsed_time(e) / reps
+        back = ss.resolve_shares_vec([sh[1], sh[2], sh[4]], [2, 3, 5], n)
+        prng[f"chacha{rounds}"] = {"ms": pm, "elems_per_s": n / (pm * 1e-3),
+                                   "hbm_GBps": n * (8 + 5 * 66) / (pm * 1e-3) / 1e9,
+                                   "roundtrip_equal": bool(torch.equal(back, sec))}
+    rows["split_prng"] = {"workload": f"3-of-5 split of 2^{log2n} int64, coefficients generated on the device "
+                                      f"(338 B/elem HBM)", **prng}
+    del sh, sec, back
     # coordinator member sum: 10 int64 members
     from delta_node.utils import sum_int64
 

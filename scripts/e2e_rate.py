@@ -10,6 +10,9 @@ elements, 3-of-5:
   B  pipelined: 2^20-element chunks; the host draws chunk c+1's coefficients
      while the GPU copies/splits/copies back chunk c (two streams).
   C  transfer ceilings: pinned H2D and D2H bandwidth alone.
+  D  device-PRNG drop-in: make_shares_vec_prng(host int64) -> H2D of the
+     secrets + split with ChaCha20 coefficients on the GPU, then D2H of the
+     shares (no host coefficient draw, no coefficient transfer).
 
 Prints one JSON object.
 """
@@ -130,4 +133,24 @@ out["B_pipelined"] = {"chunk": C, "total_s": tB, "elems_per_s": N / tB, "input_M
 a0 = field.vec_to_limbs(host_shares[0].numpy(), N)
 b0 = np.concatenate([field.vec_to_limbs(pin_out[c, 0].numpy(), C) for c in range(nch)])
 out["B_equals_A"] = bool(np.array_equal(a0, b0))
+
+# ---- D: device-PRNG drop-in -------------------------------------------------
+del pin_out, bufs
+key = bytes(range(32))
+ss.make_shares_vec_prng(torch.from_numpy(sec_h[:4096]), NS, key=key)  # warm the kernel
+sync()
+t0 = time.perf_counter()
+sec = torch.from_numpy(sec_h).to(dev)
+sync()
+t1 = time.perf_counter()
+shares, _ = ss.make_shares_vec_prng(sec, NS, key=key)
+sync()
+t2 = time.perf_counter()
+host_shares.copy_(shares)
+sync()
+t3 = time.perf_counter()
+out["D_prng_dropin"] = {"h2d_s": t1 - t0, "split_s": t2 - t1, "d2h_s": t3 - t2, "total_s": t3 - t0,
+                        "elems_per_s": N / (t3 - t0), "input_MBps": N * 8 / (t3 - t0) / 1e6,
+                        "roundtrip_equal": bool(torch.equal(
+                            ss.resolve_shares_vec([shares[0], shares[2], shares[4]], [1, 3, 5], N), sec))}
 print(json.dumps(out))
