@@ -68,13 +68,16 @@ __device__ __forceinline__ bool prng_rejected(const uint32_t v[17]) {
 }
 
 // Redraw (odds 2^-520 per coefficient; never taken in practice, kept exact).
-__device__ __attribute__((noinline)) void prng_retry(uint32_t v[17], const ChachaKey& K, uint64_t i) {
-  uint32_t blk[16];
+// Uses v itself as the block buffer: the top-limb block first (keeping word
+// 0), then the low block — no extra registers on the hot path.
+__device__ __forceinline__ void prng_retry(uint32_t v[17], const ChachaKey& K, uint64_t i) {
+#pragma unroll 1
   for (uint32_t attempt = 0;; ++attempt) {
     const uint64_t c = kRetryDomain + (i << 6) + 2ull * (attempt & 31u);
+    chacha_block(v, K, c + 1);
+    const uint32_t top = v[0] & 0x1FFu;
     chacha_block(v, K, c);
-    chacha_block(blk, K, c + 1);
-    v[16] = blk[0] & 0x1FFu;
+    v[16] = top;
     if (!prng_rejected(v)) return;
   }
 }

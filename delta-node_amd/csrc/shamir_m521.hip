@@ -72,7 +72,8 @@ __device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, u
   }
 }
 
-// D = 2 * c (a one-bit left shift across limbs; c < 2^521 so no overflow).
+// D = 2 * c (a one-bit left shift across limbs; c < 2^543 so no overflow).
+// D may alias c: limb i reads c[i] and c[i-1] before either is overwritten.
 __device__ __forceinline__ void twice(uint32_t D[kLimbs], const uint32_t c[kLimbs]) {
 #pragma unroll
   for (int i = kLimbs - 1; i > 0; --i) D[i] = __builtin_amdgcn_alignbit(c[i], c[i - 1], 31);
@@ -162,6 +163,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
         if constexpr (T == 3) {
           // hand-ordered for the headline t = 3 (58 VGPRs, 8 waves/SIMD):
           // D2 = 2 c2; c2 <- c1 + c2; c1 <- c2 + D2 (= c1 + 3 c2); c2 <- c2 + c0.
+          // (c0 is added last: an int64 secret is 2 live limbs until then.)
           uint32_t d2[kLimbs];
           twice(d2, c[2]);
           add_fe(c[2], c[1]);
