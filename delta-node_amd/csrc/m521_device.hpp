@@ -86,11 +86,12 @@ __device__ __forceinline__ void load_fe_b(rsrc_t r, uint32_t w, uint32_t v[kLimb
           kTopMask;
 }
 
+template <int AUX = kNt>
 __device__ __forceinline__ void store_fe_b(rsrc_t r, uint32_t w, const uint32_t v[kLimbs]) {
   const uint32_t o4 = w * 4u, o2 = w * 2u;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) __builtin_amdgcn_raw_buffer_store_b32(v[i], r, o4, i * 4 * kTile, kNt);
-  __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(v[16]), r, o2, static_cast<int>(kHiOffset), kNt);
+  for (int i = 0; i < 16; ++i) __builtin_amdgcn_raw_buffer_store_b32(v[i], r, o4, i * 4 * kTile, AUX);
+  __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(v[16]), r, o2, static_cast<int>(kHiOffset), AUX);
 }
 
 // ---- carry chains ----------------------------------------------------------
@@ -174,6 +175,7 @@ __device__ __forceinline__ void fd_step(uint32_t D[T][kLimbs]) {
 // If any lane of the wave needs more (odds ~2^-9 per lane), the whole wave
 // reduces D IN PLACE (same residue, smaller value: later forward differences
 // stay exact and within bounds) and stores it — no copy, no extra registers.
+template <int AUX = kNt>
 __device__ __forceinline__ void store_reduced(rsrc_t r, uint32_t w, uint32_t D[kLimbs]) {
   const uint32_t hi = D[16] >> 9;
   const uint32_t top = D[16] & kTopMask;
@@ -182,13 +184,13 @@ __device__ __forceinline__ void store_reduced(rsrc_t r, uint32_t w, uint32_t D[k
   const bool rare = (c != 0u) || (top == kTopMask);
   if (__builtin_expect(__ballot(rare) != 0ull, 0)) {
     reduce(D);
-    store_fe_b(r, w, D);
+    store_fe_b<AUX>(r, w, D);
   } else {
     const uint32_t o4 = w * 4u, o2 = w * 2u;
-    __builtin_amdgcn_raw_buffer_store_b32(l0, r, o4, 0, kNt);
+    __builtin_amdgcn_raw_buffer_store_b32(l0, r, o4, 0, AUX);
 #pragma unroll
-    for (int i = 1; i < 16; ++i) __builtin_amdgcn_raw_buffer_store_b32(D[i], r, o4, i * 4 * kTile, kNt);
-    __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(top), r, o2, static_cast<int>(kHiOffset), kNt);
+    for (int i = 1; i < 16; ++i) __builtin_amdgcn_raw_buffer_store_b32(D[i], r, o4, i * 4 * kTile, AUX);
+    __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(top), r, o2, static_cast<int>(kHiOffset), AUX);
   }
 }
 

@@ -129,7 +129,7 @@ __device__ __forceinline__ void prng_coeffs_of(const SplitArgs& a, uint32_t tile
 
 constexpr int kMaxPrngT = 8;
 
-template <int T, bool FE_SECRET, bool FOLD, bool PRNG = false>
+template <int T, bool FE_SECRET, bool FOLD, bool PRNG = false, int SAUX = kNt>
 __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nwaves = gridDim.x * kWavesPerBlock;
@@ -198,7 +198,8 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
         uint32_t (&D)[T][kLimbs] = c;
 #pragma unroll 1
         for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
-          store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), w, D[0]);
+          store_reduced<SAUX>(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), w,
+                              D[0]);
           fd_step<T>(D);
         }
       } else {
@@ -447,7 +448,16 @@ static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
   switch (t) {
     case 1: hipLaunchKernelGGL((split_kernel<1, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
     case 2: hipLaunchKernelGGL((split_kernel<2, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 3: {
+      // DN_STORE_AUX (A/B hook): cache policy bits of the share stores, headline kernel only
+      const char* sa = (!FE_SECRET && !FOLD) ? std::getenv("DN_STORE_AUX") : nullptr;
+      const int aux = sa ? std::atoi(sa) : kNt;
+      if (aux == 0) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 0>), g, dim3(kBlock), 0, s, a);
+      else if (aux == 1) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 1>), g, dim3(kBlock), 0, s, a);
+      else if (aux == 3) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 3>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a);
+      break;
+    }
     case 4: hipLaunchKernelGGL((split_kernel<4, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
     case 5: hipLaunchKernelGGL((split_kernel<5, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
     case 6: hipLaunchKernelGGL((split_kernel<6, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;

@@ -49,7 +49,7 @@ def test_split_prng_equals_split_of_materialized_coeffs(N, t, n):
     co = coeff_block(N, t - 1)
     ref = torch.empty_like(shares)
     _native.split_u64(sec, co, ref, N, t, n)
-    assert torch.equal(shares, ref)
+    assert np.array_equal(block_limbs(shares, N), block_limbs(ref, N))  # valid elements (tile tails unwritten)
     want = c_oracle.split(sec.cpu().numpy(), c_oracle.prng_coeffs(KEY, 5, 0, N, t - 1), t, n)
     assert np.array_equal(block_limbs(shares, N), want)
 
@@ -77,9 +77,11 @@ def test_make_shares_vec_prng_roundtrip_and_key():
         back = ss.resolve_shares_vec([block[x - 1] for x in xs], xs, N)
         assert torch.equal(back.cpu(), vals)
     again, _ = ss.make_shares_vec_prng(vals, 5, key=key)
-    assert torch.equal(again, block)
+    assert np.array_equal(block_limbs(again[:, : field.vec_bytes(4096)], 4096),
+                          block_limbs(block[:, : field.vec_bytes(4096)], 4096))
+    assert torch.equal(ss.resolve_shares_vec([again[0], again[1], again[3]], [1, 2, 4], N).cpu(), vals)
     other, _ = ss.make_shares_vec_prng(vals, 5, key=key, nonce=1)
-    assert not torch.equal(other, block)
+    assert not torch.equal(other[1, :4096], block[1, :4096])
     # coefficients are in [1, p-1] (spot check through the materialized stream)
     lim = block_limbs(coeff_block(4096, 2, key=key, nonce=0), 4096)
     ints = [sum(int(w) << (32 * k) for k, w in enumerate(lim[j, e])) for j in range(2) for e in range(0, 4096, 97)]
