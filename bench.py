@@ -337,7 +337,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS,
                      "traffic": (traffic or {}).get("split_bytes_per_launch"),
-                     "kernel": "dn::split_kernel<3,false,false>",
+                     "kernel": "dn::split_kernel<3, false, false, false, 2>",
                      "algorithmic_bytes_per_launch": split_bytes, "avg_launch_ms": split_ms},
         "kernels": {"split_ms": split_ms, "reconstruct_ms": recon_ms,
                     "split_GBps": achieved, "reconstruct_GBps": recon_bytes / (recon_ms * 1e-3) / 1e9,

@@ -350,7 +350,7 @@ def test_tile_map_and_grid_cap_do_not_change_results(N, cap, monkeypatch):
         _native.reconstruct([shares[1], shares[2], shares[4]], _native.lagrange([2, 3, 5], t), out_u64=rec, n=N)
         assert torch.equal(rec, secd)
         outs.append(shares)
-    assert torch.equal(outs[0], outs[1])
+    assert np.array_equal(block_limbs(outs[0], N), block_limbs(outs[1], N))  # valid elements
     s = min(N, 2048)
     co = np.stack([field.vec_to_limbs(coeffs[j, : field.vec_bytes(s)].cpu().numpy(), s) for j in range(t - 1)], axis=1)
     got = np.stack([field.vec_to_limbs(outs[1][x, : field.vec_bytes(s)].cpu().numpy(), s) for x in range(n)])
