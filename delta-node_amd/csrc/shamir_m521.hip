@@ -15,6 +15,7 @@
 // contraction), only v_mad_u64_u32 / v_add_co chains in the VALU.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -407,14 +408,31 @@ static void launch_recon_k(int k, dim3 g, hipStream_t s, const ReconArgs& a) {
   hipLaunchKernelGGL((reconstruct_kernel<A, INV, 0>), g, dim3(kBlock), 0, s, a);
 }
 
-// Workgroups per launch: each 4-wave workgroup strides over tiles; up to
-// 16384 workgroups (2^24 elements: one tile per wave; measured 1-3 % ahead
-// of 4096 on reconstruct, profiles/r01/tune_gridcap*.jsonl).
-// DN_GRID_CAP overrides it (read per call; used by scripts/tune_kernels.py).
-static int grid_for(uint64_t ntiles) {
+// Compute units of the current device (cached per device id).
+static int cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+  cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
+
+// Workgroups per launch: each 4-wave workgroup strides over tiles.
+// Default (reconstruct, compute-heavier splits): up to 16384 workgroups
+// (2^24 elements: one tile per wave; 1-3 % ahead of 4096 on reconstruct,
+// profiles/r01/tune_gridcap*.jsonl).  The write-dominated difference-table
+// split uses one workgroup per CU (one wave per SIMD, 64 tiles per wave at
+// 2^24): same time as the full grid where the share buffer's placement is
+// fast, 4-5 % faster where it is slow (fewer writes in flight through the
+// L2 / EA path; DESIGN.md §5.1, profiles/r01/placement/).
+// DN_GRID_CAP overrides both (read per call; used by the tuning scripts).
+static int grid_for(uint64_t ntiles, bool per_cu = false) {
   const char* s = std::getenv("DN_GRID_CAP");
   const int v = s ? std::atoi(s) : 0;
-  const uint64_t cap = v > 0 ? static_cast<uint64_t>(v) : 16384u;
+  const uint64_t cap = v > 0 ? static_cast<uint64_t>(v) : per_cu ? static_cast<uint64_t>(cu_count()) : 16384u;
   const uint64_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
   return static_cast<int>(blocks < cap ? blocks : cap);
 }
@@ -530,12 +548,13 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   }
   a.n_shares = n_shares;
   a.threshold = threshold;
-  const dim3 g(grid_for(a.ntiles));
-  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
-  hipStream_t s = static_cast<hipStream_t>(stream);
   // DN_SPLIT_HORNER=1 forces the Horner kernel (A/B hook, read per call).
   const char* hz = std::getenv("DN_SPLIT_HORNER");
   const bool fold_each = needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
+  const bool per_cu = !prng && !fold_each && threshold <= 8;  // the memory-bound difference-table kernels
+  const dim3 g(grid_for(a.ntiles, per_cu));
+  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
+  hipStream_t s = static_cast<hipStream_t>(stream);
   if (prng && threshold > 1) {
     if (fold_each) launch_split_prng<true>(threshold, g, s, a);
     else launch_split_prng<false>(threshold, g, s, a);
