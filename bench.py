@@ -32,6 +32,15 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+# 32-bit VALU: 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz (MI355X_MICROARCH.md: a wave64
+# VALU instruction issues over 2 cycles on its SIMD) = 78.6 T lane-ops/s
+PEAK_VALU_GOPS = 256 * 4 * 32 * 2.4
+
+
+def roof(bound: str, achieved: float, note: str) -> dict:
+    peak, unit = (PEAK_HBM_GBPS, "GB/s") if bound == "hbm" else (PEAK_VALU_GOPS, "Gop/s")
+    return {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
+            "per_unit": note}
 FE_BYTES = 66           # ceil(521 / 8): one field element in the tiled layout
 
 
@@ -123,10 +132,34 @@ def rows_bench(dev, log2n: int) -> dict:
     e.record()
     torch.cuda.synchronize()
     dec_ms = s.elapsed_time(e) / reps
+    # CPU: the reference's per-share codec (shamir.py:28-45) restated, on a 2^16 sample of the same shares
+    from oracle.py_shamir import parse_share, share_to_bytes
+
+    k = 1 << 16
+    ys = _field.vec_to_ints(blk[2, : _field.vec_bytes(k)].cpu().numpy(), k)
+    t0 = time.perf_counter()
+    recs = [share_to_bytes(3, y) for y in ys]
+    cpu_enc = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    back_ys = [parse_share(r)[1] for r in recs]
+    cpu_dec = time.perf_counter() - t0
+    enc_bytes = n * 66 + total + 8 * (n + 1)
+    dec_bytes = total + 8 * (n + 1) + n * 66 + 8 * n
     rows["share_codec"] = {"workload": f"share x=3 of 2^{log2n} elements <-> packed _share_to_bytes records",
                            "encode_ms": enc_ms, "decode_ms": dec_ms, "bytes_out": total,
                            "encode_elems_per_s": n / (enc_ms * 1e-3), "decode_elems_per_s": n / (dec_ms * 1e-3),
-                           "roundtrip_equal": bool(torch.equal(vec, blk[2]))}
+                           "roundtrip_equal": bool(torch.equal(vec, blk[2])),
+                           "reference_bytes_equal_sample": bool(
+                               b"".join(recs[:4096]) == bytes(packed[: int(offs[4096].item())].cpu().numpy())
+                               and back_ys == ys),
+                           "roofline_encode": roof("hbm", enc_bytes / (enc_ms * 1e-3) / 1e9,
+                                                   "66 B vector + record bytes + 8 B offset per element"),
+                           "roofline_decode": roof("hbm", dec_bytes / (dec_ms * 1e-3) / 1e9,
+                                                   "record bytes + 8 B offset in, 66 B + 8 B x out per element"),
+                           "cpu_baseline": {"encode_elems_per_s": k / cpu_enc, "decode_elems_per_s": k / cpu_dec,
+                                            "cores": 1, "kind": "port",
+                                            "sample": "2^16 shares, _share_to_bytes / _bytes_to_share restated "
+                                                      "(oracle/py_shamir.py), 1 core"}}
     # device-PRNG split (dn_m521_split_prng, SURVEY §8(d) config 2'): coefficients generated in-kernel
     from delta_node.crypto.shamir import _native as _nat
 
@@ -143,8 +176,12 @@ def rows_bench(dev, log2n: int) -> dict:
         torch.cuda.synchronize()
         pm = s.elapsed_time(e) / reps
         back = ss.resolve_shares_vec([sh[1], sh[2], sh[4]], [2, 3, 5], n)
+        ops = (2 * 17 / 16) * (12 * 4 * rounds + 32)  # ChaCha lane-ops per element (2.125 blocks)
         prng[f"chacha{rounds}"] = {"ms": pm, "elems_per_s": n / (pm * 1e-3),
-                                   "hbm_GBps": n * (8 + 5 * 66) / (pm * 1e-3) / 1e9,
+                                   "roofline_hbm": roof("hbm", n * (8 + 5 * 66) / (pm * 1e-3) / 1e9,
+                                                        "8 B secret + 5 x 66 B shares per element"),
+                                   "roofline_valu": roof("valu", n * ops / (pm * 1e-3) / 1e9,
+                                                         f"{ops:.0f} ChaCha lane-ops per element (2.125 blocks)"),
                                    "roundtrip_equal": bool(torch.equal(back, sec))}
     rows["split_prng"] = {"workload": f"3-of-5 split of 2^{log2n} int64, coefficients generated on the device "
                                       f"(338 B/elem HBM)", **prng}
@@ -161,9 +198,19 @@ def rows_bench(dev, log2n: int) -> dict:
     e.record()
     torch.cuda.synchronize()
     sm = s.elapsed_time(e) / reps
+    k = 1 << 22  # CPU: make_masked_results' numpy accumulation (coord/horizontal/agg.py:227-251), 1 core
+    memh = [m[:k].cpu().numpy() for m in mem]
+    t0 = time.perf_counter()
+    acc = memh[0].copy()
+    for mh in memh[1:]:
+        acc += mh
+    cpu_sum = time.perf_counter() - t0
     rows["member_sum"] = {"workload": f"10 members x 2^{log2n} int64 masked results", "ms": sm,
-                          "hbm_GBps": 11 * 8 * n / (sm * 1e-3) / 1e9,
-                          "equal_torch_sum": bool(torch.equal(outs, torch.stack(mem).sum(0)))}
+                          "roofline": roof("hbm", 11 * 8 * n / (sm * 1e-3) / 1e9, "10 x 8 B in + 8 B out per element"),
+                          "equal_torch_sum": bool(torch.equal(outs, torch.stack(mem).sum(0))),
+                          "equal_numpy_sample": bool(np.array_equal(outs[:k].cpu().numpy(), acc)),
+                          "cpu_baseline": {"elems_per_s": k / cpu_sum, "cores": 1, "kind": "port",
+                                           "sample": "2^22 elements x 10 members, numpy += (the reference's loop)"}}
     # MiMC7 data commitment (utils/mimc7.py:63-92): 2^15 rows x (9 features + label), 256 Merkle roots
     from delta_node.utils import mimc7
     from oracle import py_mimc7
@@ -181,14 +228,19 @@ def rows_bench(dev, log2n: int) -> dict:
     t0 = time.perf_counter()
     want = py_mimc7.data_commitment(data[:256])
     cdt = time.perf_counter() - t0
+    mulmods = (1 << 15) * 10 * 13 * 4 + 256 * 127 * 2 * 13 * 4  # x^7 = 4 Montgomery products per round
     rows["mimc7_commitment"] = {"workload": "calc_data_commitment, 2^15 rows x 10 cols -> 256 roots",
                                 "ms": mm, "rows_per_s": (1 << 15) / (mm * 1e-3),
+                                "mont_mul_per_s": mulmods / (mm * 1e-3),
+                                "parallelism": "one lane per row (512 waves for 1024 SIMDs), then one wave per "
+                                               "128-row Merkle block: latency-bound chains at this size",
                                 "oracle_prefix_equal": roots[:2] == want, "bound": "valu (BN254 Montgomery mul)",
                                 "cpu_python": {"rows_per_s": 256 / cdt, "sample": "256 rows, Python ints 1 thread"}}
     rows["mask_masking"] = {
         "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
         "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
-        "hbm_GBps": 16 * n / (ms * 1e-3) / 1e9, "bound": "valu (PCG64 128-bit LCG + Lemire per draw)",
+        "roofline": roof("hbm", 16 * n / (ms * 1e-3) / 1e9, "8 B float64 in + 8 B int64 out per element"),
+        "bound": "valu (PCG64 128-bit LCG step + XSL-RR + 64x64 Lemire multiply per draw)",
         "numpy_prefix_equal": ok,
         "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}
     return rows
