@@ -37,7 +37,7 @@ struct SplitArgs {
   uint64_t vec_bytes;
   uint64_t coeff_stride;  // bytes between coefficient rows (>= vec_bytes)
   uint64_t share_stride;  // bytes between share rows (>= vec_bytes)
-  uint32_t xcd_chunk;     // 1: XCD-contiguous wave numbering (grid % 8 == 0)
+  uint32_t tile_map;      // wave_sched mode (0 cyclic, 1 XCD, 2 blocked, 3 coop)
   int32_t n_shares;
   int32_t threshold;  // runtime t (generic kernel only)
   uint64_t elem_offset;  // PRNG coefficients: global index of element 0 (multiple of 256)
@@ -48,15 +48,45 @@ constexpr int kBlock = 256;  // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr uint32_t kXcds = 8;
 
-// First tile of this wave.  Workgroups are dispatched to the 8 XCDs round-
-// robin (XCD = blockIdx % 8); with xcd_chunk the grid is renumbered so that
-// XCD x works the x-th contiguous eighth of each grid-stride pass, i.e. the
-// workgroups resident on one XCD touch adjacent tiles (a footprint 8x smaller
-// per XCD L2 / translation cache) instead of every 8th block of the window.
-__device__ __forceinline__ uint32_t first_wave(uint32_t xcd_chunk) {
+// Which tiles (and which 64-element quarters q of each tile) a wave works.
+// Workgroups are dispatched to the 8 XCDs round-robin (XCD = blockIdx % 8).
+//   0 cyclic:  wave w takes tiles w, w + W, w + 2W, ... (W waves), all 4 quarters;
+//   1 XCD:     as 0, renumbered so that XCD x works the x-th contiguous eighth
+//              of each grid-stride pass (8x smaller footprint per XCD L2);
+//   2 blocked: wave w takes the contiguous run of tiles [w P, (w + 1) P);
+//   3 coop:    workgroup b takes tiles b, b + G, ...; its wave i quarter i, so
+//              the 4 waves write each 1-KB plane row of a tile together.
+struct WaveSched {
+  uint32_t first, step, end, q0, q1;
+};
+
+__device__ __forceinline__ WaveSched wave_sched(uint32_t map, uint64_t ntiles64) {
+  const uint32_t ntiles = static_cast<uint32_t>(ntiles64);
+  const uint32_t wib = threadIdx.x >> 6;
   uint32_t b = blockIdx.x;
-  if (xcd_chunk) b = (b % kXcds) * (gridDim.x / kXcds) + b / kXcds;
-  return b * kWavesPerBlock + (threadIdx.x >> 6);
+  WaveSched s{0u, 1u, ntiles, 0u, 4u};
+  if (map == 3u) {
+    s.first = b;
+    s.step = gridDim.x;
+    s.q0 = wib;
+    s.q1 = wib + 1u;
+  } else if (map == 2u) {
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    const uint32_t per = (ntiles + nw - 1u) / nw;
+    const uint32_t w = b * kWavesPerBlock + wib;
+    s.first = w * per;
+    s.end = s.first + per < ntiles ? s.first + per : ntiles;
+  } else {
+    if (map == 1u) b = (b % kXcds) * (gridDim.x / kXcds) + b / kXcds;
+    s.first = b * kWavesPerBlock + wib;
+    s.step = gridDim.x * kWavesPerBlock;
+  }
+  s.first = __builtin_amdgcn_readfirstlane(s.first);
+  s.step = __builtin_amdgcn_readfirstlane(s.step);
+  s.end = __builtin_amdgcn_readfirstlane(s.end);
+  s.q0 = __builtin_amdgcn_readfirstlane(s.q0);
+  s.q1 = __builtin_amdgcn_readfirstlane(s.q1);
+  return s;
 }
 
 template <bool FE_SECRET>
@@ -133,16 +163,15 @@ constexpr int kMaxPrngT = 8;
 template <int T, bool FE_SECRET, bool FOLD, bool PRNG = false, int SAUX = kNt>
 __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
+  const WaveSched ws = wave_sched(a.tile_map, a.ntiles);
   static_assert(!PRNG || (T >= 2 && !FE_SECRET), "PRNG coefficients: u64 secrets, t >= 2");
   // PRNG: per-wave slice of the tile's top-limb words
   __shared__ uint32_t s_tops[PRNG ? kWavesPerBlock : 1][PRNG ? 256 * (T - 1) : 1];
   uint32_t* tops = s_tops[PRNG ? (threadIdx.x >> 6) : 0];
-  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+  for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
     if constexpr (PRNG) prng_tile_tops<T>(a, tile, lane, tops);
 #pragma unroll 1
-    for (uint32_t q = 0; q < 4; ++q) {
+    for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
       const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
       if (e >= a.n_elem) break;
@@ -233,11 +262,10 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
 template <bool FE_SECRET>
 __global__ void __launch_bounds__(kBlock) split_kernel_generic(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
-  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+  const WaveSched ws = wave_sched(a.tile_map, a.ntiles);
+  for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
 #pragma unroll 1
-    for (uint32_t q = 0; q < 4; ++q) {
+    for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
       const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
       if (e >= a.n_elem) break;
@@ -268,14 +296,13 @@ __global__ void __launch_bounds__(kBlock) split_kernel_generic(const SplitArgs a
 template <int T>
 __global__ void __launch_bounds__(kBlock) prng_coeffs_kernel(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
+  const WaveSched ws = wave_sched(a.tile_map, a.ntiles);
   __shared__ uint32_t s_tops[kWavesPerBlock][256 * (T - 1)];
   uint32_t* tops = s_tops[threadIdx.x >> 6];
-  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+  for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
     prng_tile_tops<T>(a, tile, lane, tops);
 #pragma unroll 1
-    for (uint32_t q = 0; q < 4; ++q) {
+    for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
       if (static_cast<uint64_t>(tile) * kTile + w >= a.n_elem) break;
       uint32_t c[T][kLimbs];
@@ -295,7 +322,7 @@ struct ReconArgs {
   uint32_t* overflow;
   uint64_t n_elem;
   uint64_t ntiles;
-  uint32_t xcd_chunk;
+  uint32_t tile_map;
   int32_t k;
   uint32_t neg;
   uint32_t shift;
@@ -319,11 +346,10 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
   constexpr int N = A + kLimbs;
   constexpr int VB = (A == kLimbs) ? 1046 : (521 + 32 * A + 4);
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t nwaves = gridDim.x * kWavesPerBlock;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(first_wave(a.xcd_chunk));
-  for (uint32_t tile = wave0; tile < a.ntiles; tile += nwaves) {
+  const WaveSched ws = wave_sched(a.tile_map, a.ntiles);
+  for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
 #pragma unroll 1
-    for (uint32_t q = 0; q < 4; ++q) {
+    for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
       const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
       const bool valid = e < a.n_elem;
@@ -437,10 +463,15 @@ static int grid_for(uint64_t ntiles, bool per_cu = false) {
   return static_cast<int>(blocks < cap ? blocks : cap);
 }
 
-// DN_TILE_MAP=1 selects the XCD-contiguous numbering (A/B hook, read per call).
-static uint32_t xcd_chunk_for(int grid) {
+// DN_TILE_MAP=0..3 selects the wave_sched mode (A/B hook, read per call);
+// default 0.  Mode 1 needs grid % 8 == 0; the PRNG kernels (one wave per tile
+// for the shared top-limb blocks) cannot use mode 3.
+static uint32_t tile_map_for(int grid, bool allow_coop = true) {
   const char* s = std::getenv("DN_TILE_MAP");
-  return (s && s[0] == '1' && grid % static_cast<int>(kXcds) == 0) ? 1u : 0u;
+  const uint32_t m = (s && s[0] >= '0' && s[0] <= '3') ? static_cast<uint32_t>(s[0] - '0') : 0u;
+  if (m == 1u && grid % static_cast<int>(kXcds) != 0) return 0u;
+  if (m == 3u && !allow_coop) return 0u;
+  return m;
 }
 
 static int check_launch(const char* what) {
@@ -473,6 +504,10 @@ static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
       if (aux == 0) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 0>), g, dim3(kBlock), 0, s, a);
       else if (aux == 1) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 1>), g, dim3(kBlock), 0, s, a);
       else if (aux == 3) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 3>), g, dim3(kBlock), 0, s, a);
+      else if (aux == 16) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 16>), g, dim3(kBlock), 0, s, a);
+      else if (aux == 17) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 17>), g, dim3(kBlock), 0, s, a);
+      else if (aux == 18) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 18>), g, dim3(kBlock), 0, s, a);
+      else if (aux == 19) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 19>), g, dim3(kBlock), 0, s, a);
       else hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a);
       break;
     }
@@ -553,7 +588,7 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   const bool fold_each = needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
   const bool per_cu = !prng && !fold_each && threshold <= 8;  // the memory-bound difference-table kernels
   const dim3 g(grid_for(a.ntiles, per_cu));
-  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
+  a.tile_map = tile_map_for(static_cast<int>(g.x), !prng);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (prng && threshold > 1) {
     if (fold_each) launch_split_prng<true>(threshold, g, s, a);
@@ -609,7 +644,7 @@ extern "C" int dn_m521_prng_coeffs(const uint32_t* key, uint64_t nonce, int roun
   a.vec_bytes = a.ntiles * kTileBytes;
   a.coeff_stride = a.vec_bytes;
   const dim3 g(grid_for(a.ntiles));
-  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
+  a.tile_map = tile_map_for(static_cast<int>(g.x), false);
   launch_prng_coeffs(tm1 + 1, g, static_cast<hipStream_t>(stream), a);
   return check_launch("dn_m521_prng_coeffs");
 }
@@ -649,7 +684,7 @@ extern "C" int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_
   std::memcpy(a.a, w->a, sizeof(a.a));
   std::memcpy(a.inv, w->inv, sizeof(a.inv));
   const dim3 g(grid_for(a.ntiles));
-  a.xcd_chunk = xcd_chunk_for(static_cast<int>(g.x));
+  a.tile_map = tile_map_for(static_cast<int>(g.x));
   hipStream_t s = static_cast<hipStream_t>(stream);
   a.d = w->d;
   a.d_inv32 = w->d_inv32;

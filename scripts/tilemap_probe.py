@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Split / reconstruct duration per share allocation, default vs XCD-contiguous
-wave numbering (DN_TILE_MAP=0/1), interleaved in one process."""
+"""Split / reconstruct duration per share allocation under each wave schedule
+(DN_TILE_MAP=0 cyclic, 1 XCD-contiguous, 2 blocked, 3 workgroup-cooperative;
+MODES=0,1,2,3) and optional grid caps (CAPS=0,16384; 0 = library default),
+interleaved in one process so every mode sees the same allocations."""
 import json
 import os
 import sys
@@ -26,6 +28,7 @@ rec = torch.empty(N, dtype=torch.int64, device=dev)
 w135 = _native.lagrange([1, 3, 5], 3)
 sets = [torch.empty((5, field.vec_bytes(N)), dtype=torch.uint8, device=dev) for _ in range(int(os.environ.get("SETS", "6")))]
 stream = torch.cuda.current_stream()
+MODES = [f"{m}/{c}" for m in os.environ.get("MODES", "0,1,2,3").split(",") for c in os.environ.get("CAPS", "0").split(",")]
 
 
 def timed(fn, iters=8):
@@ -42,8 +45,10 @@ def timed(fn, iters=8):
 res = {}
 for rnd in range(3):
     for i, sh in enumerate(sets):
-        for m in ("0", "1"):
-            os.environ["DN_TILE_MAP"] = m
+        for m in MODES:
+            os.environ["DN_TILE_MAP"] = m.split("/")[0]
+            cap = m.split("/")[1] if "/" in m else "0"
+            os.environ["DN_GRID_CAP"] = cap
             res.setdefault((i, m, "split"), []).extend(timed(lambda: _native.split_u64(sec, coeffs, sh, N, 3, 5)))
             rows = [sh[0], sh[2], sh[4]]
             res.setdefault((i, m, "recon"), []).extend(timed(lambda: _native.reconstruct(rows, w135, out_u64=rec, n=N)))

@@ -330,9 +330,11 @@ def test_empty_and_zero_share_calls():
 @pytest.mark.parametrize("N,cap", [(256 * 4 * 64, 0), (256 * 4 * 64 + 77, 0), (256 * 4 * 64, 24), (100000, 8),
                                    (256 * 4 * 13, 0)])
 def test_tile_map_and_grid_cap_do_not_change_results(N, cap, monkeypatch):
-    """DN_TILE_MAP=1 (XCD-contiguous wave numbering; grids not a multiple of 8
-    fall back) and small grid caps (several grid-stride passes) give the same
-    shares and reconstructions as the default mapping, equal to the C oracle."""
+    """Every wave schedule DN_TILE_MAP=0..3 (cyclic, XCD-contiguous — grids not a
+    multiple of 8 fall back —, blocked runs, workgroup-cooperative quarters) and
+    small grid caps (several grid-stride passes) give the same shares and
+    reconstructions, equal to the C oracle; the device-PRNG split too (mode 3
+    falls back to 0 there)."""
     t, n = 3, 5
     sec = secrets_int64(N + cap, N)
     ss = shamir.SecretShare(t)
@@ -341,16 +343,23 @@ def test_tile_map_and_grid_cap_do_not_change_results(N, cap, monkeypatch):
     secd = torch.from_numpy(sec).to(dev())
     if cap:
         monkeypatch.setenv("DN_GRID_CAP", str(cap))
-    outs = []
-    for m in ("0", "1"):
+    outs, prng = [], []
+    key = bytes(range(32))
+    for m in ("0", "1", "2", "3"):
         monkeypatch.setenv("DN_TILE_MAP", m)
+        ps = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
+        _native.split_prng(secd, key, 7, 20, 0, ps, N, t, n)
+        prng.append(block_limbs(ps, N))
         shares = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
         _native.split_u64(secd, coeffs, shares, N, t, n)
         rec = torch.empty(N, dtype=torch.int64, device=dev())
         _native.reconstruct([shares[1], shares[2], shares[4]], _native.lagrange([2, 3, 5], t), out_u64=rec, n=N)
         assert torch.equal(rec, secd)
         outs.append(shares)
-    assert np.array_equal(block_limbs(outs[0], N), block_limbs(outs[1], N))  # valid elements
+    for o in outs[1:]:
+        assert np.array_equal(block_limbs(outs[0], N), block_limbs(o, N))  # valid elements
+    for o in prng[1:]:
+        assert np.array_equal(prng[0], o)
     s = min(N, 2048)
     co = np.stack([field.vec_to_limbs(coeffs[j, : field.vec_bytes(s)].cpu().numpy(), s) for j in range(t - 1)], axis=1)
     got = np.stack([field.vec_to_limbs(outs[1][x, : field.vec_bytes(s)].cpu().numpy(), s) for x in range(n)])
