@@ -1,0 +1,32 @@
+"""BASELINE config 5 plumbing at a small size: a masked-result round from this
+process (pack -> H2D -> split -> encode -> D2H -> HTTP) to a second local
+process over loopback, which decodes shares 1, 3, 5 on its own HIP context,
+reconstructs and checks the digest of the secrets (scripts/e2e_round.py)."""
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _e2e():
+    spec = importlib.util.spec_from_file_location("e2e_round", os.path.join(ROOT, "scripts", "e2e_round.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("coeffs", ["prng", "mt"])
+def test_masked_result_round_over_loopback(coeffs):
+    e2e = _e2e()
+    port = 18000 + os.getpid() % 1000 + (0 if coeffs == "prng" else 1000)
+    proc = e2e.start_peer(port)
+    try:
+        e2e._wait_ready(port)
+        st = e2e.run_round((1 << 14) + 77, port, coeffs=coeffs, seed=5)
+    finally:
+        e2e.stop_peer(proc, port)
+    assert st["peer_verified"]
+    assert st["bytes_posted"] > 5 * 66 * (1 << 14)
