@@ -72,6 +72,84 @@ def cpu_baseline(t: int, n: int, xs, budget_s: float, max_elems: int) -> dict:
                       f"pure-Python restatement of delta_node/crypto/shamir, {dt:.1f} s on 1 core"}
 
 
+def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int = 5) -> dict:
+    """BASELINE config 4: 5-of-9 split of a 2^26-element vector sharded by
+    element across the ranks (rank r: `dist.shard_range`), then one RCCL
+    all-gather of the per-rank share blocks (world > 1), timed separately.
+    Coefficients are materialised from the device ChaCha8 stream at each
+    rank's global element offset (dn_m521_prng_coeffs: synthetic, shard-
+    independent); the timed kernel is the same split that reads coefficients
+    (866 B/element).  Parity: every rank reconstructs its shard from shares
+    1,3,5,7,9 and compares with its secrets; after the gather, the full vector's
+    slice of every rank equals that rank's own block."""
+    from delta_node.crypto.shamir import _native, dist as sdist, field
+
+    t, n = 5, 9
+    N_total = 1 << log2n_total
+    lo, hi = sdist.shard_range(N_total, rank, world)
+    nl = hi - lo
+    B = sdist.shard_tiles(N_total, world) * field.TILE_BYTES
+    vb = field.vec_bytes(nl)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    sec = torch.randint(-(1 << 62), 1 << 62, (nl,), dtype=torch.int64, device=dev, generator=g)
+    coeffs = torch.empty((t - 1, vb), dtype=torch.uint8, device=dev)
+    _native.prng_coeffs(bytes(range(32)), 4, 8, lo, coeffs, nl, t - 1)
+    block = torch.zeros((n, B), dtype=torch.uint8, device=dev)
+    shares = block if vb == B else torch.empty((n, vb), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    for _ in range(2):
+        _native.split_u64(sec, coeffs, shares, nl, t, n)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record(stream)
+        _native.split_u64(sec, coeffs, shares, nl, t, n)
+        b.record(stream)
+    torch.cuda.synchronize()
+    split_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if shares is not block:
+        block[:, :vb].copy_(shares)
+    xs = [1, 3, 5, 7, 9]
+    rec = torch.empty(nl, dtype=torch.int64, device=dev)
+    _native.reconstruct([shares[x - 1] for x in xs], _native.lagrange(xs, t), out_u64=rec, n=nl)
+    ok = bool(torch.equal(rec, sec))
+    per_elem = 8 + (t - 1) * FE_BYTES + n * FE_BYTES
+    split_max_ms = split_ms
+    out = {"workload": f"{t}-of-{n} split of 2^{log2n_total} int64 elements sharded over {world} GPU(s), "
+                       f"2^{log2n_total} / {world} per GPU",
+           "elements_per_gpu": nl, "split_ms": split_ms,
+           "roofline": roof("hbm", nl * per_elem / (split_ms * 1e-3) / 1e9,
+                            f"8 B secret + {t - 1} x 66 B coefficients + {n} x 66 B shares per element"),
+           "roundtrip_equal": ok}
+    if world > 1:
+        import torch.distributed as tdist
+
+        tt = torch.tensor([split_ms], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        split_max_ms = float(tt.item())
+        full = sdist.allgather_share_blocks(block, N_total)  # warm-up (RCCL channels)
+        del full
+        tdist.barrier()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for _ in range(3):
+            full = sdist.allgather_share_blocks(block, N_total)
+        torch.cuda.synchronize()
+        tdist.barrier()
+        gdt = (time.perf_counter() - g0) / 3
+        same = bool(torch.equal(full[:, rank * B: rank * B + vb], block[:, :vb]))
+        del full
+        flags = torch.tensor([int(ok and same)], dtype=torch.int32, device=dev)
+        tdist.all_reduce(flags, op=tdist.ReduceOp.MIN)
+        recv = block.numel() * (world - 1)
+        out["allgather"] = {"ms": gdt * 1e3, "bytes_received_per_gpu": recv, "GBps_per_gpu": recv / gdt / 1e9,
+                            "blocks_equal": same, "all_ranks_ok": bool(flags.item())}
+    out["split_elems_per_s_aggregate"] = N_total / (split_max_ms * 1e-3)
+    del block, shares, coeffs, sec, rec
+    torch.cuda.empty_cache()
+    return out
+
+
 def rows_bench(dev, log2n: int) -> dict:
     """SURVEY §8(f) rows measured beside the headline (device-resident inputs):
     mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
@@ -267,6 +345,9 @@ def main():
     ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of share blocks (N>1)")
     ap.add_argument("--rows", type=int, default=1, help="also measure the SURVEY §8(f) rows built so far")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--config4", type=int, default=1, help="also run BASELINE config 4 (5-of-9 split of 2^26 "
+                                                            "sharded over the ranks + RCCL all-gather)")
+    ap.add_argument("--config4-log2n", type=int, default=26, help="config 4 total elements = 2^this")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -275,8 +356,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        # DN_DIST_BACKEND=gloo rehearses the multi-rank control flow on a
+        # 1-GPU box (ranks share cuda:0); the product path is nccl (RCCL).
+        backend = os.environ.get("DN_DIST_BACKEND", "nccl")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from delta_node.crypto import shamir
@@ -388,7 +476,10 @@ def main():
                    "parallelism": f"element-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS,
-                     "traffic": (traffic or {}).get("split_bytes_per_launch"),
+                     # PMC bytes of the headline launch (2^24, 3-of-5); null for other sizes
+                     "traffic": ((traffic or {}).get("split_bytes_per_launch")
+                                 if abs((traffic or {}).get("split_bytes_per_launch", 0) - split_bytes)
+                                 < 0.01 * split_bytes else None),
                      "kernel": "dn::split_kernel<3, false, false, false, 2>",
                      "algorithmic_bytes_per_launch": split_bytes, "avg_launch_ms": split_ms},
         "kernels": {"split_ms": split_ms, "reconstruct_ms": recon_ms,
@@ -398,6 +489,10 @@ def main():
     }
     if allgather:
         line["allgather"] = allgather
+    if args.config4:
+        del shares, coeffs, share_rows
+        torch.cuda.empty_cache()
+        line["config4"] = config4_bench(dev, world, rank, args.config4_log2n)
     if args.rows:
         line["rows"] = rows_bench(dev, args.log2n)
     if rank == 0 and world == 1 and args.cpu_budget > 0:
