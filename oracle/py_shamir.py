@@ -105,3 +105,31 @@ class RefSecretShare:
         for i in range(k):
             total += (nums[i] * den * ys[i] % p) * _inv(dens[i], p) % p
         return int_to_bytes(total * _inv(den, p) % p)
+
+
+def time_elements(t: int, n: int, xs: Sequence[int], budget_s: float, seed: int, max_elems: int = 1 << 22):
+    """bench.py's cpu_baseline leg: per element make_shares + resolve_shares
+    (checked) over int64 secrets from numpy PCG64(seed) until `budget_s`
+    seconds have passed.  Returns (elements done, seconds)."""
+    import time
+
+    import numpy as np
+
+    ss = RefSecretShare(t, seed=seed)
+    sec = np.random.default_rng(seed).integers(-(1 << 63), (1 << 63) - 1, size=max_elems, endpoint=True,
+                                               dtype=np.int64)
+    done = 0
+    t0 = time.perf_counter()
+    while done < max_elems:
+        v = int(sec[done]) & ((1 << 64) - 1)
+        shares = ss.make_shares(v.to_bytes(8, "big"), n)
+        out = ss.resolve_shares([shares[x - 1] for x in xs])
+        assert int.from_bytes(out, "big") == v
+        done += 1
+        if (done & 255) == 0 and time.perf_counter() - t0 > budget_s:
+            break
+    return done, time.perf_counter() - t0
+
+
+def time_elements_star(args):
+    return time_elements(*args)
