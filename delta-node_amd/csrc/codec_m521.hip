@@ -115,11 +115,26 @@ __global__ void __launch_bounds__(1024) scan_blocks_kernel(uint64_t* __restrict_
 }
 
 // One wave = 64 consecutive elements = one contiguous run of records.
+// Each lane lays its record into the wave's LDS window at its final byte
+// position (mod 4 like the destination): the 1 + xlen header bytes one by
+// one, then y.  y's minimal big-endian bytes are the tail of the 68-byte
+// big-endian image W_0..W_16 (W_m = bswap(limb 16 - m)) ending at the record
+// end E, so with r = (68 - E) mod 4 every destination dword is one
+// v_alignbyte of two neighbouring W words (static indices): dwords wholly
+// inside [y start, E) go out as ds_write_b32, the two partial edge dwords
+// byte by byte.  The window is then written to HBM as aligned dwords.
+__device__ __forceinline__ void lds_put_bytes(uint8_t* sb, int32_t lo, int32_t hi, int32_t pos, uint32_t word) {
+  // bytes of `word` (LE at LDS position pos) that fall inside [lo, hi)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (pos + i >= lo && pos + i < hi) sb[pos + i] = static_cast<uint8_t>(word >> (8 * i));
+}
+
 __global__ void __launch_bounds__(kCodecBlock) encode_kernel(const uint8_t* __restrict__ vec, uint64_t n, XBytes xb,
                                                              const uint32_t* __restrict__ local,
                                                              const uint64_t* __restrict__ block_pre,
                                                              uint64_t* __restrict__ offsets, uint8_t* __restrict__ out) {
-  __shared__ uint32_t s_buf[kCodecBlock / 64][(64 * kMaxRecord + 8) / 4 + 1];
+  __shared__ uint32_t s_buf[kCodecBlock / 64][(64 * kMaxRecord + 8) / 4 + 2];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint64_t e = (static_cast<uint64_t>(blockIdx.x) * kCodecBlock) + threadIdx.x;
   const bool valid = e < n;
@@ -142,11 +157,31 @@ __global__ void __launch_bounds__(kCodecBlock) encode_kernel(const uint8_t* __re
   const uint64_t B = __shfl(endl, last);
   const uint64_t A4 = A & ~3ull;
   uint8_t* sb = reinterpret_cast<uint8_t*>(s_buf[wv]);
+  uint32_t* sw4 = s_buf[wv];
   if (valid) {
-    uint32_t p = static_cast<uint32_t>(off - A4);
-    sb[p++] = static_cast<uint8_t>(xb.len);
-    for (uint32_t i = 0; i < xb.len; ++i) sb[p++] = xb.b[i];
-    for (int i = static_cast<int>(ylen) - 1; i >= 0; --i) sb[p++] = static_cast<uint8_t>(v[i >> 2] >> (8 * (i & 3)));
+    const int32_t p = static_cast<int32_t>(off - A4);
+    const int32_t ys = p + 1 + static_cast<int32_t>(xb.len);
+    const int32_t E = ys + static_cast<int32_t>(ylen);
+    sb[p] = static_cast<uint8_t>(xb.len);
+    for (uint32_t i = 0; i < xb.len; ++i) sb[p + 1 + i] = xb.b[i];
+    if (ylen) {
+      uint32_t W[kLimbs + 1];
+#pragma unroll
+      for (int m = 0; m < kLimbs; ++m) W[m] = __builtin_bswap32(v[kLimbs - 1 - m]);
+      W[kLimbs] = 0u;
+      const int32_t base = E - 4 * kLimbs;           // LDS position of image byte 0
+      const uint32_t r = static_cast<uint32_t>(-base) & 3u;
+      const int32_t d0 = (base + static_cast<int32_t>(r)) >> 2;  // dword holding image bytes r..r+3
+      // dword d0 - 1: image bytes 0..r-1 at its top (r > 0)
+      if (r) lds_put_bytes(sb, ys, E, 4 * (d0 - 1), __builtin_amdgcn_alignbyte(W[0], 0u, r));
+#pragma unroll
+      for (int m = 0; m < kLimbs; ++m) {
+        const uint32_t u = __builtin_amdgcn_alignbyte(W[m + 1], W[m], r);
+        const int32_t pos = 4 * (d0 + m);
+        if (pos >= ys && pos + 4 <= E) sw4[d0 + m] = u;
+        else if (pos + 4 > ys && pos < E) lds_put_bytes(sb, ys, E, pos, u);
+      }
+    }
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -170,20 +205,21 @@ __global__ void __launch_bounds__(kCodecBlock) encode_kernel(const uint8_t* __re
 // mod p (resolve_shares reduces ys the same way, shamir.py:86-88).  Records
 // whose y has more than 68 significant bytes, or whose x is longer than
 // 8 bytes, are counted in *bad and stored as 0 (the caller re-decodes them).
-__global__ void __launch_bounds__(kCodecBlock) decode_kernel(const uint8_t* __restrict__ in,
-                                                             const uint64_t* __restrict__ offsets, uint64_t n,
-                                                             uint8_t* __restrict__ vec, uint64_t* __restrict__ xs,
-                                                             uint32_t* __restrict__ bad) {
-  const uint64_t e = (static_cast<uint64_t>(blockIdx.x) * kCodecBlock) + threadIdx.x;
-  if (e >= n) return;
-  const uint64_t o = offsets[e], end = offsets[e + 1];
+//
+// One wave = 64 consecutive records = one contiguous byte window: the wave
+// stages the window in LDS with dword loads, then each lane rebuilds its limbs
+// from the record's tail: LE limb i is the big-endian dword ending 4i bytes
+// before the record end, i.e. bswap of one v_alignbyte of two LDS dwords,
+// masked to the bytes after the y start.  Windows larger than the LDS slice
+// (records padded with leading zero bytes) take the byte-serial path.
+__device__ __forceinline__ bool parse_record_global(const uint8_t* __restrict__ in, uint64_t o, uint64_t end,
+                                                    uint64_t& x, uint32_t v[kLimbs]) {
   bool ok = end > o;
   const uint32_t xlen = ok ? in[o] : 0u;
-  uint64_t x = 0;
+  x = 0;
   ok = ok && xlen <= 8 && o + 1 + xlen <= end;
   if (ok)
     for (uint32_t i = 0; i < xlen; ++i) x = (x << 8) | in[o + 1 + i];
-  uint32_t v[kLimbs];
 #pragma unroll
   for (int i = 0; i < kLimbs; ++i) v[i] = 0u;
   if (ok) {
@@ -197,10 +233,87 @@ __global__ void __launch_bounds__(kCodecBlock) decode_kernel(const uint8_t* __re
         const uint32_t byte = in[end - 1 - i];
         v[i >> 2] |= byte << (8 * (i & 3));
       }
-      reduce(v);
     }
   }
-  if (!ok) {
+  return ok;
+}
+
+constexpr int kDecPad = 8;  // LDS bytes before / after each wave's window
+constexpr int kDecWindow = 64 * kMaxRecord + 8;
+
+__global__ void __launch_bounds__(kCodecBlock) decode_kernel(const uint8_t* __restrict__ in, uint64_t in_bytes,
+                                                             const uint64_t* __restrict__ offsets, uint64_t n,
+                                                             uint8_t* __restrict__ vec, uint64_t* __restrict__ xs,
+                                                             uint32_t* __restrict__ bad) {
+  __shared__ uint32_t s_win[kCodecBlock / 64][(kDecWindow + 2 * kDecPad) / 4];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t e0 = (static_cast<uint64_t>(blockIdx.x) * kCodecBlock) + (threadIdx.x & ~63u);
+  if (e0 >= n) return;  // wave-uniform
+  const uint64_t e = e0 + lane;
+  const bool valid = e < n;
+  const uint64_t eN = e0 + 64 < n ? e0 + 64 : n;
+  const uint64_t A = offsets[e0], Bend = offsets[eN];
+  const uint64_t A4 = A & ~3ull;
+  uint64_t x = 0;
+  uint32_t v[kLimbs];
+  bool ok;
+  if (Bend >= A && Bend <= in_bytes && Bend - A4 <= static_cast<uint64_t>(kDecWindow)) {
+    uint32_t* S = s_win[wv] + kDecPad / 4;  // S[k] = dword at window byte 4k
+    uint8_t* sb = reinterpret_cast<uint8_t*>(S);
+    const uint64_t B4 = Bend & ~3ull;
+    const uint32_t nw = static_cast<uint32_t>((B4 - A4) / 4);
+    const uint32_t* inw = reinterpret_cast<const uint32_t*>(in + A4);
+    for (uint32_t q = lane; q < nw; q += 64) S[q] = __builtin_nontemporal_load(inw + q);
+    if (lane < Bend - B4) sb[B4 - A4 + lane] = in[B4 + lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    ok = false;
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) v[i] = 0u;
+    if (valid) {
+      const uint64_t oe = offsets[e], ee = offsets[e + 1];
+      // untrusted offsets: the record must lie inside this wave's window
+      ok = oe >= A && ee > oe && ee <= Bend;
+      const int32_t o = static_cast<int32_t>(oe - A4), end = static_cast<int32_t>(ee - A4);
+      const uint32_t xlen = ok ? sb[o] : 0u;
+      ok = ok && xlen <= 8 && o + 1 + static_cast<int32_t>(xlen) <= end;
+      if (ok) {
+        for (uint32_t i = 0; i < xlen; ++i) x = (x << 8) | sb[o + 1 + i];
+        int32_t ys = o + 1 + static_cast<int32_t>(xlen);
+        for (; end - ys > 68; ++ys)  // leading zero bytes beyond 68 (rare)
+          if (sb[ys]) {
+            ok = false;
+            break;
+          }
+        if (ok) {
+#pragma unroll
+          for (int i = 0; i < kLimbs; ++i) {
+            const int32_t q = end - 4 * (i + 1);        // window position of limb i's top byte
+            const int32_t nv = end - ys - 4 * i;         // bytes of limb i inside y
+            const int32_t qa = q < -4 ? -4 : q;          // stay inside the padded slice
+            const uint32_t lo = S[qa >> 2], hi = S[(qa >> 2) + 1];
+            uint32_t w = __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, static_cast<uint32_t>(qa) & 3u));
+            w = nv >= 4 ? w : (nv <= 0 ? 0u : (w & ((1u << (8 * nv)) - 1u)));
+            v[i] = w;
+          }
+        }
+      }
+    }
+  } else if (valid) {
+    const uint64_t oe = offsets[e], ee = offsets[e + 1];
+    ok = oe < ee && ee <= in_bytes && parse_record_global(in, oe, ee, x, v);
+    if (!ok) {
+#pragma unroll
+      for (int i = 0; i < kLimbs; ++i) v[i] = 0u;
+    }
+  } else {
+    ok = false;
+  }
+  if (!valid) return;
+  if (ok) {
+    reduce(v);
+  } else {
 #pragma unroll
     for (int i = 0; i < kLimbs; ++i) v[i] = 0u;
     atomicAdd(bad, 1u);
@@ -254,13 +367,13 @@ extern "C" int dn_m521_encode_shares(const void* vec, uint64_t n_elem, uint64_t 
   return DN_OK;
 }
 
-extern "C" int dn_m521_decode_shares(const uint8_t* in, const uint64_t* offsets, uint64_t n_elem, void* vec,
-                                     uint64_t* xs, uint32_t* bad_count, void* stream) {
+extern "C" int dn_m521_decode_shares(const uint8_t* in, uint64_t in_bytes, const uint64_t* offsets, uint64_t n_elem,
+                                     void* vec, uint64_t* xs, uint32_t* bad_count, void* stream) {
   if (n_elem == 0) return DN_OK;
   if (!in || !offsets || !vec || !bad_count) return set_error(DN_ERR_ARG, "dn_m521_decode_shares: null pointer");
   const uint64_t blocks = (n_elem + kCodecBlock - 1) / kCodecBlock;
   hipLaunchKernelGGL(decode_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0,
-                     static_cast<hipStream_t>(stream), in, offsets, n_elem, static_cast<uint8_t*>(vec), xs,
+                     static_cast<hipStream_t>(stream), in, in_bytes, offsets, n_elem, static_cast<uint8_t*>(vec), xs,
                      bad_count);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_m521_decode_shares: %s", hipGetErrorString(err));

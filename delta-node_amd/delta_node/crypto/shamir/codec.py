@@ -33,7 +33,7 @@ def _lib():
         L.dn_m521_encode_shares.restype = i32
         L.dn_m521_encode_shares.argtypes = [vp, u64, u64, vp, vp, u64, vp, u64, vp]
         L.dn_m521_decode_shares.restype = i32
-        L.dn_m521_decode_shares.argtypes = [vp, vp, u64, vp, vp, vp, vp]
+        L.dn_m521_decode_shares.argtypes = [vp, u64, vp, u64, vp, vp, vp, vp]
         _bound = True
     return L
 
@@ -67,7 +67,7 @@ def decode_share_vec(packed, offsets, n: int):
     vec = torch.empty(field.vec_bytes(n), dtype=torch.uint8, device=dev)
     xs = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     bad = torch.zeros(1, dtype=torch.int32, device=dev)
-    _native.check(L.dn_m521_decode_shares(packed.data_ptr(), offsets.data_ptr(), n, vec.data_ptr(), xs.data_ptr(),
+    _native.check(L.dn_m521_decode_shares(packed.data_ptr(), packed.numel(), offsets.data_ptr(), n, vec.data_ptr(), xs.data_ptr(),
                                           bad.data_ptr(), _native.stream_ptr()))
     nbad = int(bad.item())
     if nbad:

@@ -186,12 +186,14 @@ uint64_t dn_m521_encoded_capacity(uint64_t n_elem, uint64_t x);
  * (capacity >= dn_m521_encoded_capacity), device scratch. */
 int dn_m521_encode_shares(const void* vec, uint64_t n_elem, uint64_t x, uint64_t* offsets, uint8_t* out,
                           uint64_t capacity, void* scratch, uint64_t scratch_bytes, void* stream);
-/* Decode records (device in, offsets[n+1]) into a tiled vector, y reduced
- * mod p as resolve_shares does; xs (device uint64[n], may be NULL) receives
- * each record's x.  Records with x longer than 8 bytes or y longer than 68
- * bytes are counted in *bad_count (device) and decoded as 0. */
-int dn_m521_decode_shares(const uint8_t* in, const uint64_t* offsets, uint64_t n_elem, void* vec, uint64_t* xs,
-                          uint32_t* bad_count, void* stream);
+/* Decode records (device in[in_bytes], offsets[n+1]) into a tiled vector, y
+ * reduced mod p as resolve_shares does; xs (device uint64[n], may be NULL)
+ * receives each record's x.  Records with x longer than 8 bytes or y longer
+ * than 68 significant bytes, and records whose offsets are decreasing or run
+ * past in_bytes (offsets come from the wire), are counted in *bad_count
+ * (device) and decoded as 0; nothing outside in[0, in_bytes) is read. */
+int dn_m521_decode_shares(const uint8_t* in, uint64_t in_bytes, const uint64_t* offsets, uint64_t n_elem, void* vec,
+                          uint64_t* xs, uint32_t* bad_count, void* stream);
 
 /* Thread-local message of the last failure (never NULL). */
 const char* dn_last_error(void);

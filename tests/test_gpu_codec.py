@@ -96,3 +96,30 @@ def test_byte_api_fixture_through_vector_codec():
             packed, offs = codec.encode_share_vec(vec, len(ys), x)
             recs = codec.records_to_list(packed.cpu(), offs.cpu())
             assert recs[x - 1] == bytes.fromhex(case["shares"][x - 1])
+
+
+def test_decode_wide_windows_and_untrusted_offsets():
+    """Wave windows of records padded with leading zero bytes (larger than the
+    LDS slice: byte-serial path) beside normal ones, a 69-byte y with one
+    leading zero and 68 significant bytes, and offsets a peer got wrong
+    (decreasing / out of range: flagged, never read outside the input)."""
+    rng = random.Random(11)
+    ys = [rng.randrange(1 << 544) for _ in range(300)]
+    recs = []
+    for i, y in enumerate(ys):
+        yb = y.to_bytes((y.bit_length() + 7) // 8, "big")
+        pad = 100 if 64 <= i < 128 else (1 if i % 7 == 0 else 0)
+        recs.append(bytes([1, 4]) + b"\x00" * pad + yb)
+    packed = torch.tensor(list(b"".join(recs)), dtype=torch.uint8, device=dev())
+    offs = torch.tensor(np.cumsum([0] + [len(r) for r in recs]), dtype=torch.int64, device=dev())
+    vec, xs = codec.decode_share_vec(packed, offs, len(recs))
+    assert field.vec_to_ints(vec.cpu().numpy(), len(recs)) == [y % P for y in ys]
+    assert torch.equal(xs.cpu(), torch.full((len(recs),), 4, dtype=torch.int64))
+    bad_offs = offs.clone()
+    bad_offs[10] = bad_offs[12] + 5  # record 10 runs past record 11's start, record 11 goes backwards
+    with pytest.raises(ValueError):
+        codec.decode_share_vec(packed, bad_offs, len(recs))
+    far = offs.clone()
+    far[-1] = far[-1] + (1 << 40)  # last record claims bytes far past the input
+    with pytest.raises(ValueError):
+        codec.decode_share_vec(packed, far, len(recs))
