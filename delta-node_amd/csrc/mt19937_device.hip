@@ -1,0 +1,352 @@
+// mt19937_device.hip — CPython's MT19937 coefficient draw on the GPU, bit-exact.
+//
+// Reference: SecretShare.make_shares draws its t-1 coefficients per element
+// with self.random.randint(1, p-1) (delta_node/crypto/shamir/shamir.py:59-61):
+// 1 + getrandbits(521), redrawn while >= p-1; getrandbits(521) is 17 MT19937
+// words, little-endian, the last >> 23.  dn_mt19937_draw_coeffs (host_m521.cpp)
+// restates that stream sequentially; this file produces the same values on the
+// device by cutting the word stream into substreams of kMtJumpL words:
+//
+//  * host: the MT state at the start of each substream by jump-ahead — Horner
+//    evaluation of g(f) on the 624-word window with g = x^J mod P, P the
+//    characteristic polynomial of the one-word transition f (polynomials for
+//    J = kMtJumpL - 624 and 2^k kMtJumpL precomputed by tools/gen_mt_jump.py);
+//    substream windows are built by doubling (each from an earlier one by one
+//    jump), the jumps of a doubling level spread over host threads;
+//  * device: one wave per substream keeps its window in LDS, twists it block
+//    by block (the three dependency phases of the 624-word twist, 64 lanes
+//    wide), tempers into an LDS ring and turns every complete 17-word group
+//    that starts in its substream into one coefficient (+1, rejection test)
+//    stored in the tiled layout;
+//  * host: the final CPython state (array + index) by stepping the nearest
+//    substream window forward, so self.random continues exactly as after n
+//    sequential make_shares calls.
+// A rejected draw (probability ~2^-520 per coefficient) shifts every later
+// word; the device flags it and the caller redoes the draw on the host.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "dn_internal.hpp"
+#include "m521_device.hpp"
+
+namespace dn {
+namespace {
+
+#include "mt19937_jump.inc"
+
+constexpr int kMtN = 624, kMtM = 397;
+constexpr uint32_t kMtA = 0x9908b0dfu, kMtUp = 0x80000000u, kMtLo = 0x7fffffffu;
+constexpr int kMtRing = 1024;  // tempered-word ring (>= 624 + 16)
+constexpr int kMtMaxSub = 1 << kMtJumpLevels;
+
+__host__ __device__ inline uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+__host__ __device__ inline uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
+  const uint32_t y = (a & kMtUp) | (b & kMtLo);
+  return m ^ (y >> 1) ^ ((0u - (y & 1u)) & kMtA);
+}
+
+// ------------------------------------------------------------------- host
+// A window (x_T .. x_T+623) as a ring: logical word j is w[(head + j) % 624].
+struct Ring {
+  uint32_t w[kMtN];
+  int head = 0;
+  void step() {  // -> (x_T+1 .. x_T+624)
+    const int h1 = head + 1 == kMtN ? 0 : head + 1;
+    const int hm = head + kMtM >= kMtN ? head + kMtM - kMtN : head + kMtM;
+    w[head] = mt_mix(w[head], w[h1], w[hm]);
+    head = h1;
+  }
+  void to_linear(uint32_t* out) const {
+    for (int j = 0; j < kMtN; ++j) out[j] = w[(head + j) % kMtN];
+  }
+};
+
+// out = g(f)(win): window jumped by J words, g = x^J mod P.  The low 31 bits
+// of out[0] are not determined (they never reach an output or the dynamics).
+void mt_jump(const uint32_t* win, const uint64_t* g, uint32_t* out) {
+  Ring r;
+  std::memset(r.w, 0, sizeof(r.w));
+  int top = kMtPolyWords * 64 - 1;
+  while (top >= 0 && !((g[top >> 6] >> (top & 63)) & 1u)) --top;
+  for (int i = top; i >= 0; --i) {
+    r.step();
+    if ((g[i >> 6] >> (i & 63)) & 1u) {
+      // r_logical[j] ^= win[j]: two contiguous segments of the ring
+      const int n1 = kMtN - r.head;
+      uint32_t* a = r.w + r.head;
+      for (int j = 0; j < n1; ++j) a[j] ^= win[j];
+      for (int j = 0; j < r.head; ++j) r.w[j] ^= win[n1 + j];
+    }
+  }
+  r.to_linear(out);
+}
+
+void mt_advance(const uint32_t* win, uint64_t steps, uint32_t* out) {
+  Ring r;
+  std::memcpy(r.w, win, sizeof(r.w));
+  for (uint64_t i = 0; i < steps; ++i) r.step();
+  r.to_linear(out);
+}
+
+// ----------------------------------------------------------------- device
+struct MtArgs {
+  const uint32_t* windows;  // [subs][624]; window 0 = CPython's array at time B
+  uint8_t* coeffs;          // tm1 tiled vectors
+  uint32_t* flag;           // != 0: a draw was rejected
+  uint64_t n_elem, ncoef, vb;
+  uint32_t idx;             // CPython index: stream words 0..623-idx are temper(window0[idx..])
+  int32_t tm1;
+};
+
+__global__ void __launch_bounds__(64) mt_coeffs_kernel(const MtArgs a) {
+  __shared__ uint32_t S[kMtN];
+  __shared__ uint32_t R[kMtRing];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t sub = blockIdx.x;
+  const uint64_t lo = sub * kMtJumpL, hi = lo + kMtJumpL;
+  uint64_t k = (lo + 16) / 17;                                   // first coefficient starting here
+  const uint64_t k_end = (hi + 16) / 17 < a.ncoef ? (hi + 16) / 17 : a.ncoef;
+  if (k >= k_end) return;
+  const uint32_t* win = a.windows + sub * kMtN;
+  for (int j = lane; j < kMtN; j += 64) S[j] = win[j];
+  uint64_t re;  // stream position one past the last word in the ring
+  if (sub == 0) {
+    const uint32_t h = kMtN - a.idx;
+    for (uint32_t j = lane; j < h; j += 64) R[j] = mt_temper(S[a.idx + j]);
+    re = h;
+  } else {
+    re = lo;
+  }
+  __syncthreads();
+  while (k < k_end) {
+    if (re < 17 * k + 17) {
+      // twist S in place (CPython order: three phases, reads before writes in each round)
+      for (int r = 0; r < 4; ++r) {  // k in [0, 227): reads S[k + 1], S[k + 397] (old)
+        const int kk = r * 64 + static_cast<int>(lane);
+        uint32_t v = 0;
+        if (kk < kMtN - kMtM) v = mt_mix(S[kk], S[kk + 1], S[kk + kMtM]);
+        __syncthreads();
+        if (kk < kMtN - kMtM) S[kk] = v;
+        __syncthreads();
+      }
+      for (int r = 0; r < 4; ++r) {  // k in [227, 454): S[k - 227] new (phase 1)
+        const int kk = kMtN - kMtM + r * 64 + static_cast<int>(lane);
+        uint32_t v = 0;
+        if (kk < 2 * (kMtN - kMtM)) v = mt_mix(S[kk], S[kk + 1], S[kk - (kMtN - kMtM)]);
+        __syncthreads();
+        if (kk < 2 * (kMtN - kMtM)) S[kk] = v;
+        __syncthreads();
+      }
+      for (int r = 0; r < 3; ++r) {  // k in [454, 623): S[k - 227] new (previous phase)
+        const int kk = 2 * (kMtN - kMtM) + r * 64 + static_cast<int>(lane);
+        uint32_t v = 0;
+        if (kk < kMtN - 1) v = mt_mix(S[kk], S[kk + 1], S[kk - (kMtN - kMtM)]);
+        __syncthreads();
+        if (kk < kMtN - 1) S[kk] = v;
+        __syncthreads();
+      }
+      if (lane == 0) S[kMtN - 1] = mt_mix(S[kMtN - 1], S[0], S[kMtM - 1]);
+      __syncthreads();
+      for (int j = lane; j < kMtN; j += 64) R[(re + j) & (kMtRing - 1)] = mt_temper(S[j]);
+      re += kMtN;
+      __syncthreads();
+    }
+    const uint64_t kav = re / 17 < k_end ? re / 17 : k_end;  // coefficients complete in the ring
+    for (uint64_t base = k; base < kav; base += 64) {
+      const uint64_t kk = base + lane;
+      if (kk < kav) {
+        uint32_t v[kLimbs];
+        const uint64_t w0 = 17 * kk;
+#pragma unroll
+        for (int i = 0; i < kLimbs; ++i) v[i] = R[(w0 + i) & (kMtRing - 1)];
+        v[16] >>= 23;
+        bool rej = v[16] == 0x1FFu && v[0] >= 0xFFFFFFFEu;
+#pragma unroll
+        for (int i = 1; i < 16; ++i) rej = rej && v[i] == 0xFFFFFFFFu;
+        if (rej) atomicOr(a.flag, 1u);
+        uint32_t c = 1u;  // + 1 (randint's lower bound); v < p - 1: no carry out of limb 16
+#pragma unroll
+        for (int i = 0; i < kLimbs; ++i) {
+          const uint64_t s = static_cast<uint64_t>(v[i]) + c;
+          v[i] = static_cast<uint32_t>(s);
+          c = static_cast<uint32_t>(s >> 32);
+        }
+        const uint64_t e = kk / static_cast<uint64_t>(a.tm1);
+        const uint64_t j = kk - e * static_cast<uint64_t>(a.tm1);
+        uint8_t* tb = a.coeffs + j * a.vb + (e / kTile) * kTileBytes;
+        const uint32_t w = static_cast<uint32_t>(e % kTile);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) reinterpret_cast<uint32_t*>(tb)[i * kTile + w] = v[i];
+        reinterpret_cast<uint16_t*>(tb + kHiOffset)[w] = static_cast<uint16_t>(v[16]);
+      }
+    }
+    k = kav;
+    __syncthreads();
+  }
+}
+
+// Window 1 + d (time B + (1 + d) L - h) from window 1 by the binary
+// decomposition of d (jumps of 2^k L; beyond the table, repeated top jumps).
+void mt_window_from1(const uint32_t* w1, uint64_t d, uint32_t* out) {
+  std::vector<uint32_t> cur(w1, w1 + kMtN), nxt(kMtN);
+  for (int lev = 0; d; ++lev, d >>= 1) {
+    if (lev == kMtJumpLevels - 1) {  // the rest: d times 2^lev L
+      for (uint64_t r = 0; r < d; ++r) {
+        mt_jump(cur.data(), kMtJumpPolys[1 + lev], nxt.data());
+        cur.swap(nxt);
+      }
+      break;
+    }
+    if (d & 1u) {
+      mt_jump(cur.data(), kMtJumpPolys[1 + lev], nxt.data());
+      cur.swap(nxt);
+    }
+  }
+  std::memcpy(out, cur.data(), kMtN * sizeof(uint32_t));
+}
+
+uint64_t mt_subs(uint64_t ncoef) {
+  const uint64_t words = 17 * ncoef;
+  return words ? (words + kMtJumpL - 1) / kMtJumpL : 0;
+}
+
+}  // namespace
+}  // namespace dn
+
+using namespace dn;
+
+// Stream words are numbered from CPython's current position: words
+// 0 .. h-1 (h = 624 - index) are the rest of the current array, word w >= h
+// is output w - h of the window at time B (the current array).  After W words
+// CPython holds the window at time B + 624 q (q = ceil((W - h) / 624)
+// twists) with index W - h - 624 (q - 1).
+extern "C" int dn_mt19937_skip(uint32_t* mt_state, int32_t* mt_index, uint64_t words) {
+  if (!mt_state || !mt_index) return set_error(DN_ERR_ARG, "dn_mt19937_skip: null pointer");
+  const int32_t idx = *mt_index;
+  if (idx < 0 || idx > kMtN) return set_error(DN_ERR_ARG, "dn_mt19937_skip: bad MT index");
+  const uint64_t h = static_cast<uint64_t>(kMtN - idx);
+  if (words <= h) {
+    *mt_index = idx + static_cast<int32_t>(words);
+    return DN_OK;
+  }
+  const uint64_t m_end = words - h, q = (m_end + kMtN - 1) / kMtN, tf = kMtN * q + h;
+  const uint64_t sig = (tf - 1) / kMtJumpL;
+  std::vector<uint32_t> w(kMtN), fin(kMtN);
+  uint64_t t_sig = h;
+  if (sig == 0) {
+    std::memcpy(w.data(), mt_state, kMtN * sizeof(uint32_t));
+  } else {
+    std::vector<uint32_t> adv(kMtN), w1(kMtN);
+    mt_advance(mt_state, static_cast<uint64_t>(idx), adv.data());
+    mt_jump(adv.data(), kMtJumpPolys[0], w1.data());
+    mt_window_from1(w1.data(), sig - 1, w.data());
+    t_sig = sig * kMtJumpL;
+  }
+  mt_advance(w.data(), tf - t_sig, fin.data());
+  std::memcpy(mt_state, fin.data(), kMtN * sizeof(uint32_t));
+  *mt_index = static_cast<int32_t>(m_end - kMtN * (q - 1));
+  return DN_OK;
+}
+
+extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
+  const uint64_t subs = tm1 > 0 ? mt_subs(n_elem * static_cast<uint64_t>(tm1)) : 0;
+  return 256 + subs * kMtN * 4;
+}
+
+extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1,
+                                             void* coeffs, void* scratch, uint64_t scratch_bytes, void* stream) {
+  if (!mt_state || !mt_index) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
+  if (tm1 < 0 || tm1 >= DN_MAX_THRESHOLD)
+    return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: t-1=%d", tm1);
+  const int32_t idx = *mt_index;
+  if (idx < 0 || idx > kMtN) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: bad MT index");
+  const uint64_t ncoef = n_elem * static_cast<uint64_t>(tm1);
+  if (ncoef == 0) return DN_OK;
+  if (!coeffs || !scratch) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
+  const uint64_t subs = mt_subs(ncoef);
+  if (subs > static_cast<uint64_t>(kMtMaxSub))
+    return set_error(DN_ERR_UNSUPPORTED, "dn_mt19937_draw_coeffs_device: %llu words exceed the jump table",
+                     static_cast<unsigned long long>(17 * ncoef));
+  if (scratch_bytes < dn_mt19937_device_scratch_bytes(n_elem, tm1))
+    return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: scratch too small");
+  const uint64_t W = 17 * ncoef, h = static_cast<uint64_t>(kMtN - idx);
+
+  // substream windows: 0 = CPython's array (time B); 1 = time B + L - h;
+  // 1 + d (d >= 1) = window 1 + d - 2^k jumped by 2^k L, 2^k <= d < 2^(k+1)
+  std::vector<uint32_t> wins(subs * kMtN);
+  std::memcpy(wins.data(), mt_state, kMtN * sizeof(uint32_t));
+  if (subs > 1) {
+    std::vector<uint32_t> adv(kMtN);
+    mt_advance(mt_state, static_cast<uint64_t>(idx), adv.data());
+    mt_jump(adv.data(), kMtJumpPolys[0], wins.data() + kMtN);
+  }
+  unsigned hw = std::thread::hardware_concurrency();
+  const unsigned nthr = hw ? (hw < 16 ? hw : 16) : 1;
+  for (int lev = 0; (1ull << lev) < subs - 1 && subs > 2; ++lev) {
+    const uint64_t d0 = 1ull << lev, d1 = (2ull << lev) < subs - 1 ? (2ull << lev) : subs - 1;
+    const uint64_t cnt = d1 - d0;  // windows 1 + d for d in [d0, d1)
+    auto work = [&](unsigned t) {
+      for (uint64_t i = t; i < cnt; i += nthr) {
+        const uint64_t d = d0 + i;
+        mt_jump(wins.data() + (1 + d - d0) * kMtN, kMtJumpPolys[1 + lev], wins.data() + (1 + d) * kMtN);
+      }
+    };
+    if (cnt < 4 || nthr == 1) {
+      work(0);
+      for (unsigned t = 1; t < nthr; ++t) work(t);
+    } else {
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < nthr; ++t) th.emplace_back(work, t);
+      for (auto& x : th) x.join();
+    }
+  }
+
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint8_t* sc = static_cast<uint8_t*>(scratch);
+  uint32_t* flag = reinterpret_cast<uint32_t*>(sc);
+  uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + 256);
+  hipError_t err = hipMemsetAsync(flag, 0, 4, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(dwin, wins.data(), wins.size() * 4, hipMemcpyHostToDevice, s);
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: %s", hipGetErrorString(err));
+  MtArgs a{dwin, static_cast<uint8_t*>(coeffs), flag, n_elem, ncoef, dn_m521_vec_bytes(n_elem),
+           static_cast<uint32_t>(idx), tm1};
+  hipLaunchKernelGGL(mt_coeffs_kernel, dim3(static_cast<uint32_t>(subs)), dim3(64), 0, s, a);
+  err = hipGetLastError();
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: launch: %s", hipGetErrorString(err));
+
+  // final CPython state while the device works
+  std::vector<uint32_t> fin(kMtN);
+  int32_t fidx;
+  if (W <= h) {
+    std::memcpy(fin.data(), mt_state, kMtN * 4);
+    fidx = idx + static_cast<int32_t>(W);
+  } else {
+    const uint64_t m_end = W - h, q = (m_end + kMtN - 1) / kMtN;  // q twists
+    // window at time B + 624 q from the last substream window strictly before it
+    const uint64_t tf = kMtN * q + h;  // (time - B) + h
+    uint64_t sig = (tf - 1) / kMtJumpL;
+    if (sig > subs - 1) sig = subs - 1;
+    const uint64_t t_sig = sig == 0 ? h : sig * kMtJumpL;  // (T_sig - B) + h
+    mt_advance(wins.data() + sig * kMtN, tf - t_sig, fin.data());
+    fidx = static_cast<int32_t>(m_end - kMtN * (q - 1));
+  }
+  uint32_t hflag = 0;
+  err = hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: %s", hipGetErrorString(err));
+  if (hflag) return set_error(DN_ERR_RETRY, "dn_mt19937_draw_coeffs_device: a draw was rejected; redo on the host");
+  std::memcpy(mt_state, fin.data(), kMtN * 4);
+  *mt_index = fidx;
+  return DN_OK;
+}

@@ -25,6 +25,7 @@ DN_ERR_DISTINCT = -4
 DN_ERR_HIP = -5
 DN_ERR_UNSUPPORTED = -6
 DN_ERR_EMPTY = -7
+DN_ERR_RETRY = -8
 
 MAX_RESOLVE = 16
 MAX_THRESHOLD = 64
@@ -38,6 +39,7 @@ EXPORTS = (
     "dn_m521_vec_bytes", "dn_m521_split_u64", "dn_m521_split_fe", "dn_m521_lagrange",
     "dn_m521_reconstruct", "dn_mt19937_draw_coeffs", "dn_last_error", "dn_version",
     "dn_m521_split_prng", "dn_m521_prng_coeffs",
+    "dn_mt19937_device_scratch_bytes", "dn_mt19937_draw_coeffs_device", "dn_mt19937_skip",
 )
 
 
@@ -103,6 +105,13 @@ def lib() -> ctypes.CDLL:
         L.dn_mt19937_draw_coeffs.restype = i32
         L.dn_mt19937_draw_coeffs.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64,
                                              i32, vp]
+        L.dn_mt19937_device_scratch_bytes.restype = u64
+        L.dn_mt19937_device_scratch_bytes.argtypes = [u64, i32]
+        L.dn_mt19937_draw_coeffs_device.restype = i32
+        L.dn_mt19937_draw_coeffs_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
+                                                    u64, i32, vp, vp, u64, vp]
+        L.dn_mt19937_skip.restype = i32
+        L.dn_mt19937_skip.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64]
         L.dn_last_error.restype = ctypes.c_char_p
         L.dn_last_error.argtypes = []
         L.dn_version.restype = ctypes.c_char_p
@@ -230,6 +239,44 @@ def mt_draw_coeffs(rng, n: int, tm1: int) -> np.ndarray:
     check(lib().dn_mt19937_draw_coeffs(state, ctypes.byref(index), n, tm1, out.ctypes.data))
     rng.setstate((version, tuple(state) + (index.value,), gauss))
     return out.reshape(tm1, vb)
+
+
+def _mt_state(rng):
+    version, internal, gauss = rng.getstate()
+    return version, gauss, (ctypes.c_uint32 * 624)(*internal[:624]), ctypes.c_int32(internal[624])
+
+
+def mt_skip(rng, words: int) -> None:
+    """Advance `rng` (a random.Random) by `words` 32-bit outputs by jump-ahead."""
+    version, gauss, state, index = _mt_state(rng)
+    check(lib().dn_mt19937_skip(state, ctypes.byref(index), int(words)))
+    rng.setstate((version, tuple(state) + (index.value,), gauss))
+
+
+def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
+    """`mt_draw_coeffs` with the coefficients generated on the GPU into `out`
+    (uint8 device tensor [tm1, vec_bytes(n)]), bit-exact; `rng` advances
+    identically.  Returns False (rng untouched) when the draw must be redone on
+    the host: a rejected 521-bit draw (odds ~2^-520 each) or a stream beyond
+    the jump table."""
+    import torch
+
+    if tm1 <= 0 or n == 0:
+        return True
+    vb = vec_bytes(n)
+    if out.dtype != torch.uint8 or tuple(out.shape) != (tm1, vb) or not out.is_contiguous() or not out.is_cuda:
+        raise ValueError(f"mt_draw_coeffs_device: out must be a contiguous uint8 device tensor [{tm1}, {vb}]")
+    L = lib()
+    sb = int(L.dn_mt19937_device_scratch_bytes(n, tm1))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=out.device)
+    version, gauss, state, index = _mt_state(rng)
+    rc = L.dn_mt19937_draw_coeffs_device(state, ctypes.byref(index), n, tm1, out.data_ptr(), scratch.data_ptr(), sb,
+                                         stream_ptr())
+    if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
+        return False
+    check(rc)
+    rng.setstate((version, tuple(state) + (index.value,), gauss))
+    return True
 
 
 def version() -> str:

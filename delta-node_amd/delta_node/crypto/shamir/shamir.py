@@ -29,6 +29,7 @@ call raises.  Only the default prime (the Mersenne prime M521) is supported;
 """
 from __future__ import annotations
 
+import os
 import random
 from functools import reduce
 from typing import List, Optional, Sequence, Tuple, Union
@@ -199,7 +200,17 @@ class SecretShare(object):
         import torch
 
         dev = device if device is not None else _device()
-        host = _native.mt_draw_coeffs(self.random, n, max(self.threshold, 1) - 1)
+        tm1 = max(self.threshold, 1) - 1
+        if tm1 > 0 and n > 0 and os.environ.get("DN_MT_DEVICE", "1") != "0":
+            # bit-exact MT19937 on the GPU (jump-ahead substreams); the host
+            # draw below is the fallback for a rejected draw (odds ~2^-520)
+            vb = field.vec_bytes(n)
+            blk = torch.empty((tm1, vb), dtype=torch.uint8, device=dev)
+            if n % field.TILE:
+                blk[:, vb - field.TILE_BYTES:].zero_()  # padding lanes of the last tile, as the host draw leaves them
+            if _native.mt_draw_coeffs_device(self.random, n, tm1, blk):
+                return blk
+        host = _native.mt_draw_coeffs(self.random, n, tm1)
         return torch.from_numpy(host).to(dev)
 
     def make_shares_vec(self, values, shares: int, *, coeffs=None, out=None):

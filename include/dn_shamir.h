@@ -59,7 +59,8 @@ enum {
   DN_ERR_DISTINCT = -4,    /* shamir.py:74-75  "shares must be distinct"           */
   DN_ERR_HIP = -5,         /* HIP runtime error (launch failure)                   */
   DN_ERR_UNSUPPORTED = -6, /* outside the limits above                             */
-  DN_ERR_EMPTY = -7        /* shamir.py:78-83  k == 1: reduce() of empty iterable  */
+  DN_ERR_EMPTY = -7,       /* shamir.py:78-83  k == 1: reduce() of empty iterable  */
+  DN_ERR_RETRY = -8        /* device MT draw hit a rejected draw: redo on the host */
 };
 
 /* Bytes of one tiled field-element vector of n elements (66 * round_up(n, 256)). */
@@ -170,6 +171,27 @@ int dn_m521_reconstruct(const void* const* share_vecs, const dn_m521_lagrange_t*
  */
 int dn_mt19937_draw_coeffs(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem,
                            int tm1, void* coeffs);
+
+/*
+ * The same draw, bit-exact, with the coefficients generated on the GPU
+ * (csrc/mt19937_device.hip): the host computes the MT state at the start of
+ * every 17*2^16-word substream by jump-ahead, one wave per substream runs
+ * MT19937 from there.  `coeffs` is a DEVICE block of t-1 tiled vectors,
+ * `scratch` device memory of dn_mt19937_device_scratch_bytes(n, t-1) bytes.
+ * Synchronises `stream`.  On DN_OK the state is advanced exactly as the host
+ * draw advances it.  DN_ERR_RETRY (a draw >= p-1 was seen: later words shift,
+ * odds ~2^-520 per coefficient) and DN_ERR_UNSUPPORTED (more than 4096
+ * substreams) leave the state untouched: draw on the host instead.
+ */
+uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1);
+int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1,
+                                  void* coeffs, void* scratch, uint64_t scratch_bytes, void* stream);
+
+/*
+ * Host.  Advance a CPython MT19937 state by `words` 32-bit outputs (as
+ * `words` getrandbits(32) calls would) by jump-ahead instead of stepping.
+ */
+int dn_mt19937_skip(uint32_t* mt_state, int32_t* mt_index, uint64_t words);
 
 /*
  * Share wire codec over whole vectors (shamir.py:28-45 `_share_to_bytes` /

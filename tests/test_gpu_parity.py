@@ -364,3 +364,34 @@ def test_tile_map_and_grid_cap_do_not_change_results(N, cap, monkeypatch):
     co = np.stack([field.vec_to_limbs(coeffs[j, : field.vec_bytes(s)].cpu().numpy(), s) for j in range(t - 1)], axis=1)
     got = np.stack([field.vec_to_limbs(outs[1][x, : field.vec_bytes(s)].cpu().numpy(), s) for x in range(n)])
     assert np.array_equal(got, c_oracle.split(sec[:s], co, t, n))
+
+
+@pytest.mark.parametrize("n,tm1,pre", [(1, 2, 0), (1000, 2, 3), (40000, 2, 624), (40000, 4, 100),
+                                       (100003, 1, 7), (1 << 20, 2, 0), ((1 << 20) + 77, 3, 555)])
+def test_device_mt_draw_equals_host_draw(n, tm1, pre):
+    """dn_mt19937_draw_coeffs_device (jump-ahead substreams of 17*2^16 words,
+    one wave each) gives the host draw's block byte for byte — the reference's
+    randint(1, p-1) sequence — and leaves random.Random in the same state;
+    `pre` words drawn first put CPython's index mid-array."""
+    a = random.Random(2024 + n)
+    if pre:
+        a.getrandbits(32 * pre)
+    b = random.Random()
+    b.setstate(a.getstate())
+    want = _native.mt_draw_coeffs(a, n, tm1)
+    got = torch.zeros((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    assert _native.mt_draw_coeffs_device(b, n, tm1, got)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert a.getstate() == b.getstate()
+
+
+def test_draw_coeffs_vec_device_path_matches_reference_fixture():
+    """draw_coeffs_vec (device MT by default) reproduces the coefficients the
+    reference consumed for F1 (tests/golden), and the split from them matches."""
+    f1 = load_npz("f1_t3n5.npz")
+    man = manifest()["f1"]
+    ss = shamir.SecretShare(man["t"])
+    ss.random.seed(man["mt_seed"])
+    co = ss.draw_coeffs_vec(man["N"], dev())
+    got = np.stack([field.vec_to_limbs(co[j].cpu().numpy(), man["N"]) for j in range(man["t"] - 1)], axis=1)
+    assert np.array_equal(got, f1["coeff_limbs"])

@@ -220,3 +220,25 @@ def test_no_cpu_fallback():
         ss.make_shares(b"\x07", 3)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ss.make_shares_vec(torch.arange(10, dtype=torch.int64), 3)
+
+
+@pytest.mark.parametrize("start_words", [0, 5, 623, 624, 1000])
+def test_mt19937_skip_matches_cpython(start_words):
+    """dn_mt19937_skip (jump-ahead: Horner of x^J mod P on the 624-word window,
+    polynomials from tools/gen_mt_jump.py) lands on exactly the state CPython
+    reaches by generating the words — across the head of the current array,
+    block boundaries and several 17*2^16-word jump units."""
+    L = 17 * (1 << 16)
+    for words in (0, 1, 17, 600, 624, 625, 5000, L - 1, L, L + 624, 3 * L + 12345, 7 * L + 1):
+        a = random.Random(99)
+        a.getrandbits(32 * start_words) if start_words else None
+        b = random.Random()
+        b.setstate(a.getstate())
+        _native.mt_skip(a, words)
+        left = words
+        while left:
+            take = min(left, 1 << 20)
+            b.getrandbits(32 * take)
+            left -= take
+        assert a.getstate() == b.getstate(), words
+        assert a.getrandbits(64) == b.getrandbits(64)

@@ -104,6 +104,46 @@ __global__ void __launch_bounds__(256) recon_mem(const uint8_t* __restrict__ y0,
   }
 }
 
+// recon_mem with 16 B per lane: lane l of a wave reads elements 4l..4l+3 of
+// each limb plane of a tile (one 1-KB run per wave-instruction), 4 elements
+// per lane, one share row at a time (the reconstruct's read pattern widened)
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x4v __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) recon_mem_x4(const uint8_t* __restrict__ y0, const uint8_t* __restrict__ y1,
+                                                    const uint8_t* __restrict__ y2, int64_t* __restrict__ out,
+                                                    uint32_t ntiles) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nwaves = gridDim.x * 4;
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  for (uint32_t tile = wave0; tile < ntiles; tile += nwaves) {
+    u32x4v lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
+    const uint8_t* rows[3] = {y0, y1, y2};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const uint8_t* tb = tile_base(rows[s], tile);
+      u32x4v a[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        a[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(tb + i * 4 * kTile) + lane);
+      const u16x4v t = __builtin_nontemporal_load(reinterpret_cast<const u16x4v*>(tb + kHiOffset) + lane);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        lo ^= a[i];
+        hi += a[i];
+      }
+      hi.x += t.x;
+      hi.y += t.y;
+      hi.z += t.z;
+      hi.w += t.w;
+    }
+    int64_t* o = out + (uint64_t)tile * kTile + 4 * lane;
+    __builtin_nontemporal_store((int64_t)(((uint64_t)hi.x << 32) | lo.x), o + 0);
+    __builtin_nontemporal_store((int64_t)(((uint64_t)hi.y << 32) | lo.y), o + 1);
+    __builtin_nontemporal_store((int64_t)(((uint64_t)hi.z << 32) | lo.z), o + 2);
+    __builtin_nontemporal_store((int64_t)(((uint64_t)hi.w << 32) | lo.w), o + 3);
+  }
+}
+
 template <typename F>
 static float time_ms(F f, int reps) {
   hipEvent_t a, b;
@@ -150,6 +190,11 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, N * 8));
   CHECK(hipMemset(sec, 3, N * 8));
   CHECK(hipMemset(co, 5, 2 * vb));
+  for (int grid : {1024, 2048, 4096, 16384}) {
+    float rx = time_ms([&] { recon_mem_x4<<<grid, 256>>>(sh, sh + 2 * vb, sh + 4 * vb, out, ntiles); }, reps);
+    float rr2 = time_ms([&] { recon_mem<<<grid, 256>>>(sh, sh + 2 * vb, sh + 4 * vb, out, ntiles); }, reps);
+    std::printf("{\"grid\": %d, \"recon_mem_x4_ms\": %.4f, \"recon_mem_ms\": %.4f}\n", grid, rx, rr2);
+  }
   for (int grid : {2048, 4096, 16384}) {
     float s = time_ms([&] { split_mem<<<grid, 256>>>(sec, co, sh, ntiles, vb, 5); }, reps);
     float rr = time_ms([&] { recon_mem<<<grid, 256>>>(sh, sh + 2 * vb, sh + 4 * vb, out, ntiles); }, reps);
