@@ -74,20 +74,43 @@ struct Ring {
 
 // out = g(f)(win): window jumped by J words, g = x^J mod P.  The low 31 bits
 // of out[0] are not determined (they never reach an output or the dynamics).
+// Horner over 8-bit chunks of g: r = f^8(r) ^ T[chunk], T[b] = sum_j b_j f^j(win)
+// (256 precomputed windows), so a 624-word XOR per 8 coefficients instead of
+// one per set coefficient.
+void xor_into(Ring& r, const uint32_t* lin) {  // r_logical[j] ^= lin[j]
+  const int n1 = kMtN - r.head;
+  uint32_t* a = r.w + r.head;
+  for (int j = 0; j < n1; ++j) a[j] ^= lin[j];
+  for (int j = 0; j < r.head; ++j) r.w[j] ^= lin[n1 + j];
+}
+
 void mt_jump(const uint32_t* win, const uint64_t* g, uint32_t* out) {
+  constexpr int kQ = 8;
+  std::vector<uint32_t> T(static_cast<size_t>(1 << kQ) * kMtN, 0u);
+  {
+    Ring p;
+    std::memcpy(p.w, win, sizeof(p.w));
+    for (int j = 0; j < kQ; ++j) {  // T[2^j + b] = f^j(win) ^ T[b]
+      uint32_t fj[kMtN];
+      p.to_linear(fj);
+      const int bit = 1 << j;
+      for (int b = 0; b < bit; ++b) {
+        uint32_t* d = T.data() + static_cast<size_t>(bit + b) * kMtN;
+        const uint32_t* src = T.data() + static_cast<size_t>(b) * kMtN;
+        for (int i = 0; i < kMtN; ++i) d[i] = src[i] ^ fj[i];
+      }
+      p.step();
+    }
+  }
   Ring r;
   std::memset(r.w, 0, sizeof(r.w));
   int top = kMtPolyWords * 64 - 1;
   while (top >= 0 && !((g[top >> 6] >> (top & 63)) & 1u)) --top;
-  for (int i = top; i >= 0; --i) {
-    r.step();
-    if ((g[i >> 6] >> (i & 63)) & 1u) {
-      // r_logical[j] ^= win[j]: two contiguous segments of the ring
-      const int n1 = kMtN - r.head;
-      uint32_t* a = r.w + r.head;
-      for (int j = 0; j < n1; ++j) a[j] ^= win[j];
-      for (int j = 0; j < r.head; ++j) r.w[j] ^= win[n1 + j];
-    }
+  for (int c = top / kQ; c >= 0; --c) {
+    for (int i = 0; i < kQ; ++i) r.step();
+    const int bit0 = c * kQ;
+    const uint32_t chunk = static_cast<uint32_t>((g[bit0 >> 6] >> (bit0 & 63)) & ((1u << kQ) - 1u));
+    if (chunk) xor_into(r, T.data() + static_cast<size_t>(chunk) * kMtN);
   }
   r.to_linear(out);
 }
@@ -109,6 +132,15 @@ struct MtArgs {
   int32_t tm1;
 };
 
+// The workgroup is one wave: LDS traffic between its lanes needs ordering,
+// not a hardware barrier (a wavefront-scope fence keeps the compiler from
+// moving LDS accesses across it; the LDS executes a wave's accesses in order).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ void __launch_bounds__(64) mt_coeffs_kernel(const MtArgs a) {
   __shared__ uint32_t S[kMtN];
   __shared__ uint32_t R[kMtRing];
@@ -128,7 +160,7 @@ __global__ void __launch_bounds__(64) mt_coeffs_kernel(const MtArgs a) {
   } else {
     re = lo;
   }
-  __syncthreads();
+  wave_sync();
   while (k < k_end) {
     if (re < 17 * k + 17) {
       // twist S in place (CPython order: three phases, reads before writes in each round)
@@ -136,31 +168,31 @@ __global__ void __launch_bounds__(64) mt_coeffs_kernel(const MtArgs a) {
         const int kk = r * 64 + static_cast<int>(lane);
         uint32_t v = 0;
         if (kk < kMtN - kMtM) v = mt_mix(S[kk], S[kk + 1], S[kk + kMtM]);
-        __syncthreads();
+        wave_sync();
         if (kk < kMtN - kMtM) S[kk] = v;
-        __syncthreads();
+        wave_sync();
       }
       for (int r = 0; r < 4; ++r) {  // k in [227, 454): S[k - 227] new (phase 1)
         const int kk = kMtN - kMtM + r * 64 + static_cast<int>(lane);
         uint32_t v = 0;
         if (kk < 2 * (kMtN - kMtM)) v = mt_mix(S[kk], S[kk + 1], S[kk - (kMtN - kMtM)]);
-        __syncthreads();
+        wave_sync();
         if (kk < 2 * (kMtN - kMtM)) S[kk] = v;
-        __syncthreads();
+        wave_sync();
       }
       for (int r = 0; r < 3; ++r) {  // k in [454, 623): S[k - 227] new (previous phase)
         const int kk = 2 * (kMtN - kMtM) + r * 64 + static_cast<int>(lane);
         uint32_t v = 0;
         if (kk < kMtN - 1) v = mt_mix(S[kk], S[kk + 1], S[kk - (kMtN - kMtM)]);
-        __syncthreads();
+        wave_sync();
         if (kk < kMtN - 1) S[kk] = v;
-        __syncthreads();
+        wave_sync();
       }
       if (lane == 0) S[kMtN - 1] = mt_mix(S[kMtN - 1], S[0], S[kMtM - 1]);
-      __syncthreads();
+      wave_sync();
       for (int j = lane; j < kMtN; j += 64) R[(re + j) & (kMtRing - 1)] = mt_temper(S[j]);
       re += kMtN;
-      __syncthreads();
+      wave_sync();
     }
     const uint64_t kav = re / 17 < k_end ? re / 17 : k_end;  // coefficients complete in the ring
     for (uint64_t base = k; base < kav; base += 64) {
@@ -192,7 +224,7 @@ __global__ void __launch_bounds__(64) mt_coeffs_kernel(const MtArgs a) {
       }
     }
     k = kav;
-    __syncthreads();
+    wave_sync();
   }
 }
 
