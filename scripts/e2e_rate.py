@@ -13,6 +13,10 @@ elements, 3-of-5:
   D  device-PRNG drop-in: make_shares_vec_prng(host int64) -> H2D of the
      secrets + split with ChaCha20 coefficients on the GPU, then D2H of the
      shares (no host coefficient draw, no coefficient transfer).
+  E  the bit-exact drop-in as shipped: make_shares_vec(host int64) with the
+     reference's MT19937 coefficients drawn on the GPU (jump-ahead
+     substreams, dn_mt19937_draw_coeffs_device), then D2H; the shares equal
+     A's byte for byte.
 
 Prints one JSON object.
 """
@@ -80,6 +84,7 @@ t3 = time.perf_counter()
 host_shares.copy_(shares)
 sync()
 t4 = time.perf_counter()
+host_shares_a = host_shares.clone()
 out["A_dropin"] = {"mt_draw_s": t1 - t0, "h2d_s": t2 - t1, "split_s": t3 - t2, "d2h_s": t4 - t3,
                    "total_s": t4 - t0, "elems_per_s": N / (t4 - t0), "input_MBps": N * 8 / (t4 - t0) / 1e6}
 del coeffs, shares
@@ -153,4 +158,28 @@ out["D_prng_dropin"] = {"h2d_s": t1 - t0, "split_s": t2 - t1, "d2h_s": t3 - t2, 
                         "elems_per_s": N / (t3 - t0), "input_MBps": N * 8 / (t3 - t0) / 1e6,
                         "roundtrip_equal": bool(torch.equal(
                             ss.resolve_shares_vec([shares[0], shares[2], shares[4]], [1, 3, 5], N), sec))}
+
+# ---- E: bit-exact drop-in, MT19937 drawn on the device ----------------------
+ss.random.seed(1)
+sync()
+t0 = time.perf_counter()
+sec = torch.from_numpy(sec_h).to(dev)
+sync()
+t1 = time.perf_counter()
+coeffs = ss.draw_coeffs_vec(N, dev)
+sync()
+t2 = time.perf_counter()
+shares = ss.make_shares_vec(sec, NS, coeffs=coeffs)
+sync()
+t3 = time.perf_counter()
+e_shares = torch.empty((NS, vb), dtype=torch.uint8, pin_memory=True)
+t3b = time.perf_counter()
+e_shares.copy_(shares)
+sync()
+t4 = time.perf_counter()
+out["E_mt_device_dropin"] = {"h2d_s": t1 - t0, "mt_draw_device_s": t2 - t1, "split_s": t3 - t2,
+                             "d2h_s": t4 - t3b, "total_s": (t4 - t3b) + (t3 - t0),
+                             "elems_per_s": N / ((t4 - t3b) + (t3 - t0)),
+                             "input_MBps": N * 8 / ((t4 - t3b) + (t3 - t0)) / 1e6,
+                             "equals_A": bool(torch.equal(e_shares, host_shares_a))}
 print(json.dumps(out))
