@@ -151,6 +151,43 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
     return out
 
 
+def config5_bench(log2n: int, rounds: int = 2) -> dict:
+    """BASELINE config 5: end-to-end masked-result round between this process
+    and a second local delta-node process over loopback HTTP
+    (scripts/e2e_round.py: pack -> H2D -> split -> GPU share encode -> D2H ->
+    POST per share; the peer decodes + reconstructs and checks a digest after
+    each round).  Both coefficient sources: the reference's MT19937 stream
+    drawn on the GPU (bit-exact drop-in) and the device ChaCha20 form."""
+    import importlib.util
+    import socket
+
+    spec = importlib.util.spec_from_file_location("e2e_round", os.path.join(ROOT, "scripts", "e2e_round.py"))
+    e2e = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(e2e)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    proc = e2e.start_peer(port)
+    out = {"workload": f"masked result {{'w': {{'w': int64[2^{log2n}]}}}} -> 3-of-5 shares as _share_to_bytes records, "
+                       "POSTed to a second local process over loopback HTTP; wall-clock pack start -> last HTTP 200",
+           "unit": "MB/s of int64 input"}
+    try:
+        e2e._wait_ready(port)
+        e2e.run_round(1 << 12, port, coeffs="prng")  # warm-up (peer imports torch, kernels load)
+        for coeffs in ("mt", "prng"):
+            runs = [e2e.run_round(1 << log2n, port, coeffs=coeffs, seed=r + 1) for r in range(rounds)]
+            best = max(runs, key=lambda r: r["input_MBps"])
+            out[coeffs] = {"input_MBps": best["input_MBps"], "wall_s": best["wall_s"],
+                           "wall_s_all": [r["wall_s"] for r in runs],
+                           "stages_s": {k: best[k] for k in ("pack_s", "h2d_s", "split_s", "encode_d2h_s",
+                                                             "post_tail_s")},
+                           "http_GBps": best["http_GBps"], "bytes_posted": best["bytes_posted"],
+                           "peer_verified": all(r["peer_verified"] for r in runs)}
+    finally:
+        e2e.stop_peer(proc, port)
+    return out
+
+
 def rows_bench(dev, log2n: int) -> dict:
     """SURVEY §8(f) rows measured beside the headline (device-resident inputs):
     mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
@@ -350,6 +387,8 @@ def main():
     ap.add_argument("--config4", type=int, default=1, help="also run BASELINE config 4 (5-of-9 split of 2^26 "
                                                             "sharded over the ranks + RCCL all-gather)")
     ap.add_argument("--config4-log2n", type=int, default=26, help="config 4 total elements = 2^this")
+    ap.add_argument("--config5", type=int, default=1, help="also run BASELINE config 5 (end-to-end round over "
+                                                            "loopback HTTP to a second process; N=1 only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -497,6 +536,8 @@ def main():
         line["config4"] = config4_bench(dev, world, rank, args.config4_log2n)
     if args.rows:
         line["rows"] = rows_bench(dev, args.log2n)
+    if args.config5 and world == 1:
+        line["config5"] = config5_bench(args.log2n)
     if rank == 0 and world == 1 and args.cpu_budget > 0:
         line["cpu_baseline"] = cpu_baseline(t, n, xs, args.cpu_budget)
     if rank == 0:
