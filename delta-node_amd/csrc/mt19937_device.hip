@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -377,7 +378,11 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
   err = hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s);
   if (err == hipSuccess) err = hipStreamSynchronize(s);
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: %s", hipGetErrorString(err));
-  if (hflag) return set_error(DN_ERR_RETRY, "dn_mt19937_draw_coeffs_device: a draw was rejected; redo on the host");
+  // DN_MT_FORCE_RETRY=1 (test hook) takes the rejected-draw exit so the
+  // caller's host fallback can be exercised.
+  const char* fr = std::getenv("DN_MT_FORCE_RETRY");
+  if (hflag || (fr && fr[0] == '1'))
+    return set_error(DN_ERR_RETRY, "dn_mt19937_draw_coeffs_device: a draw was rejected; redo on the host");
   std::memcpy(mt_state, fin.data(), kMtN * 4);
   *mt_index = fidx;
   return DN_OK;

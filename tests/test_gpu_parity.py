@@ -395,3 +395,22 @@ def test_draw_coeffs_vec_device_path_matches_reference_fixture():
     co = ss.draw_coeffs_vec(man["N"], dev())
     got = np.stack([field.vec_to_limbs(co[j].cpu().numpy(), man["N"]) for j in range(man["t"] - 1)], axis=1)
     assert np.array_equal(got, f1["coeff_limbs"])
+
+
+def test_device_mt_draw_falls_back_to_host_on_retry(monkeypatch):
+    """The rejected-draw exit (DN_ERR_RETRY, forced by the test hook) leaves the
+    state untouched and draw_coeffs_vec redoes the draw on the host: same block,
+    same final state as the host draw."""
+    n = 50000
+    a, b = random.Random(77), random.Random(77)
+    want = _native.mt_draw_coeffs(a, n, 2)
+    monkeypatch.setenv("DN_MT_FORCE_RETRY", "1")
+    blk = torch.zeros((2, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    state0 = b.getstate()
+    assert not _native.mt_draw_coeffs_device(b, n, 2, blk)
+    assert b.getstate() == state0
+    ss = shamir.SecretShare(3)
+    ss.random.setstate(state0)
+    got = ss.draw_coeffs_vec(n, dev())
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert ss.random.getstate() == a.getstate()
