@@ -53,3 +53,52 @@ def allgather_share_blocks(local_block, n_total: int, group=None):
     gathered = torch.empty((world * S, B), dtype=local_block.dtype, device=local_block.device)
     dist.all_gather_into_tensor(gathered, local_block.contiguous(), group=group)
     return gathered.view(world, S, B).permute(1, 0, 2).reshape(S, world * B)
+
+
+def draw_coeffs_sharded(ss, n_total: int, device=None, group=None):
+    """This rank's slice of the coefficients `ss.draw_coeffs_vec(n_total)`
+    would draw — the reference's MT19937 stream (shamir.py:59-61), bit-exact —
+    without any rank drawing the others' words: each rank jumps to its shard's
+    first word (dn_mt19937_skip) and draws only its tiles; every rank's
+    `ss.random` ends as after the whole draw.  A rejected 521-bit draw in any
+    shard (odds ~2^-520 each) shifts the later shards: the ranks agree on it
+    (one all-reduce of a flag) and then each redraws the whole stream on the
+    host and keeps its slice, so the result is exact either way.
+
+    Returns uint8 [t-1, shard_tiles(n_total, world) * TILE_BYTES] (padded like
+    `allgather_share_blocks` expects; the elements are shard_range's)."""
+    import random
+
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    lo, hi = shard_range(n_total, rank, world)
+    tm1 = max(ss.threshold, 1) - 1
+    B = shard_tiles(n_total, world) * field.TILE_BYTES
+    state0 = ss.random.getstate()
+    out = torch.zeros((tm1, B), dtype=torch.uint8, device=device)
+    if hi > lo and tm1 > 0:
+        blk = ss.draw_coeffs_vec(hi - lo, device, elem_offset=lo, n_total=n_total)
+        out[:, : blk.shape[1]].copy_(blk)
+        rejected = ss.last_draw_rejected
+    else:
+        from . import _native
+
+        _native.mt_skip(ss.random, 17 * tm1 * n_total)
+        rejected = False
+    flag = torch.tensor([int(rejected)], dtype=torch.int32, device=out.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        from . import _native
+
+        rng = random.Random()
+        rng.setstate(state0)
+        full = _native.mt_draw_coeffs(rng, n_total, tm1)  # every word, in order: exact with rejections
+        ss.random.setstate(rng.getstate())
+        t0 = lo // field.TILE
+        nb = field.vec_bytes(hi - lo) if hi > lo else 0
+        out.zero_()
+        if nb:
+            out[:, :nb].copy_(torch.from_numpy(full[:, t0 * field.TILE_BYTES: t0 * field.TILE_BYTES + nb]))
+    return out

@@ -156,6 +156,7 @@ class SecretShare(object):
         self.threshold = threshold
         self.prime = prime
         self.random = random.Random()
+        self.last_draw_rejected = False
 
     # ---- reference byte API -------------------------------------------
     def make_shares(self, value: bytes, shares: int) -> List[bytes]:
@@ -193,25 +194,52 @@ class SecretShare(object):
         return serialize.int_to_bytes(field.vec_to_ints(out.cpu().numpy(), 1)[0])
 
     # ---- vector extension (the hot path) -------------------------------
-    def draw_coeffs_vec(self, n: int, device=None):
+    def draw_coeffs_vec(self, n: int, device=None, *, elem_offset: int = 0, n_total: Optional[int] = None):
         """The (t-1) x n coefficients that n sequential `make_shares` calls
         would draw from `self.random` (advancing it identically), as a uint8
-        device tensor [t-1, vec_bytes(n)] in the tiled layout."""
+        device tensor [t-1, vec_bytes(n)] in the tiled layout.
+
+        Sharded form (elem_offset / n_total): the coefficients of elements
+        [elem_offset, elem_offset + n) of an n_total-element draw — the words
+        before the shard are skipped by jump-ahead (dn_mt19937_skip) — and
+        `self.random` ends as after the whole n_total-element draw.  Exact
+        unless a 521-bit draw is rejected (odds ~2^-520 each) in the skipped
+        range; `self.last_draw_rejected` reports one in this shard's range, and
+        `dist.draw_coeffs_sharded` combines the flags over ranks."""
         import torch
 
         dev = device if device is not None else _device()
         tm1 = max(self.threshold, 1) - 1
-        if tm1 > 0 and n > 0 and os.environ.get("DN_MT_DEVICE", "1") != "0":
+        sharded = elem_offset != 0 or (n_total is not None and n_total != n)
+        if sharded:
+            if n_total is None or not 0 <= elem_offset <= elem_offset + n <= n_total:
+                raise ValueError("draw_coeffs_vec: shard [elem_offset, elem_offset + n) must lie in [0, n_total)")
+            rng = random.Random()
+            rng.setstate(self.random.getstate())
+            _native.mt_skip(rng, 17 * tm1 * elem_offset)
+        else:
+            rng = self.random
+        self.last_draw_rejected = False
+        blk = None
+        if tm1 > 0 and n > 0 and torch.device(dev).type == "cuda" and os.environ.get("DN_MT_DEVICE", "1") != "0":
             # bit-exact MT19937 on the GPU (jump-ahead substreams); the host
             # draw below is the fallback for a rejected draw (odds ~2^-520)
             vb = field.vec_bytes(n)
             blk = torch.empty((tm1, vb), dtype=torch.uint8, device=dev)
             if n % field.TILE:
                 blk[:, vb - field.TILE_BYTES:].zero_()  # padding lanes of the last tile, as the host draw leaves them
-            if _native.mt_draw_coeffs_device(self.random, n, tm1, blk):
-                return blk
-        host = _native.mt_draw_coeffs(self.random, n, tm1)
-        return torch.from_numpy(host).to(dev)
+            if not _native.mt_draw_coeffs_device(rng, n, tm1, blk):
+                blk = None
+        if blk is None:
+            probe = random.Random()
+            probe.setstate(rng.getstate())
+            host = _native.mt_draw_coeffs(rng, n, tm1)
+            _native.mt_skip(probe, 17 * tm1 * n)
+            self.last_draw_rejected = probe.getstate() != rng.getstate()  # a rejection consumed extra words
+            blk = torch.from_numpy(host).to(dev)
+        if sharded:
+            _native.mt_skip(self.random, 17 * tm1 * n_total)
+        return blk
 
     def make_shares_vec(self, values, shares: int, *, coeffs=None, out=None):
         """Split every element of an int64 tensor.

@@ -118,3 +118,50 @@ def test_allreduce_masked_partial_sums_wrap_like_numpy():
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=10) is True
+
+
+def _mt_shard_worker(rank, world, port, N, t, q):
+    import random
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "delta-node_amd"))
+    from delta_node.crypto import shamir
+    from delta_node.crypto.shamir import _native
+    from delta_node.crypto.shamir import dist as sd
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ss = shamir.SecretShare(t)
+        ss.random.seed(4242)
+        ss.random.getrandbits(32 * 77)  # start mid-array
+        start = ss.random.getstate()
+        blk = sd.draw_coeffs_sharded(ss, N, device="cpu")
+        full = sd.allgather_share_blocks(blk, N)
+        ref = random.Random()
+        ref.setstate(start)
+        want = _native.mt_draw_coeffs(ref, N, t - 1)  # the whole stream on one host, in order
+        ok = np.array_equal(full[:, : want.shape[1]].numpy(), want) and ss.random.getstate() == ref.getstate()
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,t", [(2, 1000, 3), (3, 70001, 3), (2, 40000, 5)])
+def test_sharded_mt_draw_equals_one_stream(world, N, t):
+    """dist.draw_coeffs_sharded: every rank jumps to its shard of the
+    reference's MT19937 coefficient stream and draws only that; the gathered
+    blocks equal one sequential draw and every rank's random.Random ends in the
+    sequential draw's state (host draw path; the device path is the gpu tests')."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mt_shard_worker, args=(r, world, port, N, t, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    res = [q.get(timeout=10) for _ in range(world)]
+    assert all(ok for _, ok in res), res

@@ -414,3 +414,19 @@ def test_device_mt_draw_falls_back_to_host_on_retry(monkeypatch):
     got = ss.draw_coeffs_vec(n, dev())
     assert np.array_equal(got.cpu().numpy(), want)
     assert ss.random.getstate() == a.getstate()
+
+
+@pytest.mark.parametrize("N,lo,hi", [(1 << 20, 0, 1 << 19), (1 << 20, 1 << 19, 1 << 20), (300001, 256 * 400, 300001)])
+def test_device_mt_draw_shard_equals_slice_of_full_draw(N, lo, hi):
+    """draw_coeffs_vec(elem_offset, n_total) on the device: the shard's tiles of
+    the one-stream draw, and random.Random as after the whole n_total draw."""
+    ss_full, ss_shard = shamir.SecretShare(3), shamir.SecretShare(3)
+    ss_full.random.seed(N + lo)
+    ss_shard.random.seed(N + lo)
+    full = ss_full.draw_coeffs_vec(N, dev())
+    blk = ss_shard.draw_coeffs_vec(hi - lo, dev(), elem_offset=lo, n_total=N)
+    t0 = lo // field.TILE
+    want = full[:, t0 * field.TILE_BYTES: t0 * field.TILE_BYTES + blk.shape[1]]
+    assert np.array_equal(block_limbs(blk, hi - lo), block_limbs(want.contiguous(), hi - lo))
+    assert ss_shard.random.getstate() == ss_full.random.getstate()
+    assert not ss_shard.last_draw_rejected
