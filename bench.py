@@ -77,10 +77,9 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
     """BASELINE config 4: 5-of-9 split of a 2^26-element vector sharded by
     element across the ranks (rank r: `dist.shard_range`), then one RCCL
     all-gather of the per-rank share blocks (world > 1), timed separately.
-    Coefficients are materialised from the device ChaCha8 stream at each
-    rank's global element offset (dn_m521_prng_coeffs: synthetic, shard-
-    independent); the timed kernel is the same split that reads coefficients
-    (866 B/element).  Parity: every rank reconstructs its shard from shares
+    Coefficients are the reference's own MT19937 stream for the whole vector,
+    each rank drawing its shard on the GPU (so the gathered shares are the
+    unsharded reference split's); the timed kernel reads them (866 B/element).  Parity: every rank reconstructs its shard from shares
     1,3,5,7,9 and compares with its secrets; after the gather, the full vector's
     slice of every rank equals that rank's own block."""
     from delta_node.crypto.shamir import _native, dist as sdist, field
@@ -94,8 +93,17 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     sec = torch.randint(-(1 << 62), 1 << 62, (nl,), dtype=torch.int64, device=dev, generator=g)
-    coeffs = torch.empty((t - 1, vb), dtype=torch.uint8, device=dev)
-    _native.prng_coeffs(bytes(range(32)), 4, 8, lo, coeffs, nl, t - 1)
+    # the reference's MT19937 coefficient stream of ONE 2^26-element draw, each
+    # rank drawing only its shard on its GPU (jump-ahead; dist.draw_coeffs_sharded)
+    from delta_node.crypto import shamir as _shamir
+
+    ss = _shamir.SecretShare(t)
+    ss.random.seed(4321)
+    if world > 1:
+        cb = sdist.draw_coeffs_sharded(ss, N_total, dev)
+        coeffs = cb[:, :vb].contiguous() if cb.shape[1] != vb else cb
+    else:
+        coeffs = ss.draw_coeffs_vec(N_total, dev)
     block = torch.zeros((n, B), dtype=torch.uint8, device=dev)
     shares = block if vb == B else torch.empty((n, vb), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
