@@ -365,6 +365,11 @@ def rows_bench(dev, log2n: int) -> dict:
         "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
         "roofline": roof("hbm", 16 * n / (ms * 1e-3) / 1e9, "8 B float64 in + 8 B int64 out per element"),
         "bound": "valu (PCG64 128-bit LCG step + XSL-RR + 64x64 Lemire multiply per draw)",
+        # 49.6 VALU instructions per draw: the ISA of bounded_acc_kernel's
+        # 16-draw loop body (793 VALU), 14 of them half-rate 32x32->64
+        # multiplies (tools/valu_rates.hip: mad_u64 at ~0.57x the add rate)
+        "roofline_valu": roof("valu", 10 * n / (ms * 1e-3) * 49.6 / 1e9,
+                              "49.6 VALU instructions per draw (ISA count), 10 draws per element"),
         "numpy_prefix_equal": ok,
         "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}
     return rows
