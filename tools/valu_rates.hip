@@ -92,6 +92,42 @@ __global__ void k_fma64(uint32_t* out, uint32_t s) {
   if (r == 1.2345) out[0] = 1;
 }
 
+__global__ void k_perm(uint32_t* out, uint32_t s) {
+  uint32_t v[kChains];
+  for (int c = 0; c < kChains; ++c) v[c] = threadIdx.x + c;
+  BODY(asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(v[c]) : "v"(s)));
+  uint32_t r = 0;
+  for (int c = 0; c < kChains; ++c) r ^= v[c];
+  if (r == 0x1234567u) out[0] = r;
+}
+
+__global__ void k_lshl_or(uint32_t* out, uint32_t s) {
+  uint32_t v[kChains];
+  for (int c = 0; c < kChains; ++c) v[c] = threadIdx.x + c;
+  BODY(asm volatile("v_lshl_or_b32 %0, %0, %1, %0" : "+v"(v[c]) : "v"(s)));
+  uint32_t r = 0;
+  for (int c = 0; c < kChains; ++c) r ^= v[c];
+  if (r == 0x1234567u) out[0] = r;
+}
+
+__global__ void k_add3(uint32_t* out, uint32_t s) {
+  uint32_t v[kChains];
+  for (int c = 0; c < kChains; ++c) v[c] = threadIdx.x + c;
+  BODY(asm volatile("v_add3_u32 %0, %0, %1, %0" : "+v"(v[c]) : "v"(s)));
+  uint32_t r = 0;
+  for (int c = 0; c < kChains; ++c) r ^= v[c];
+  if (r == 0x1234567u) out[0] = r;
+}
+
+__global__ void k_addc(uint32_t* out, uint32_t s) {
+  uint32_t v[kChains];
+  for (int c = 0; c < kChains; ++c) v[c] = threadIdx.x + c;
+  BODY(asm volatile("v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(v[c]) : "v"(s) : "vcc"));
+  uint32_t r = 0;
+  for (int c = 0; c < kChains; ++c) r ^= v[c];
+  if (r == 0x1234567u) out[0] = r;
+}
+
 template <typename K>
 static void run(const char* name, K k, int ops_per_body) {
   uint32_t* out;
@@ -124,5 +160,9 @@ int main() {
   run("v_mul_hi_u32", k_mul_hi, 1);
   run("v_mad_u64_u32", k_mad64, 1);
   run("v_fma_f64", k_fma64, 1);
+  run("v_perm_b32", k_perm, 1);
+  run("v_lshl_or_b32", k_lshl_or, 1);
+  run("v_add3_u32", k_add3, 1);
+  run("v_addc_co_u32", k_addc, 1);
   return 0;
 }
