@@ -1,9 +1,20 @@
 // dn_internal.hpp — shared declarations of the native library (not part of the C-ABI).
 #pragma once
 
+#include <cstdint>
+
 #include "dn_shamir.h"
 
 namespace dn {
 // Record a thread-local error message and return `code` (printf-style).
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+// MT19937 jump-ahead (host_mt_jump.cpp): substream length in words, the most
+// substreams the jump table covers, substream start windows and CPython's
+// final state after `words` outputs (wins may be null).
+uint64_t mt_jump_words();
+uint64_t mt_jump_max_subs();
+void mt_build_windows(const uint32_t* state, int idx, uint64_t subs, uint32_t* wins);
+void mt_final_state(const uint32_t* state, int idx, uint64_t words, const uint32_t* wins, uint64_t subs,
+                    uint32_t* fin, int32_t* fidx);
 }  // namespace dn

@@ -28,7 +28,6 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <thread>
 #include <vector>
 
 #include "dn_internal.hpp"
@@ -37,12 +36,9 @@
 namespace dn {
 namespace {
 
-#include "mt19937_jump.inc"
-
 constexpr int kMtN = 624, kMtM = 397;
 constexpr uint32_t kMtA = 0x9908b0dfu, kMtUp = 0x80000000u, kMtLo = 0x7fffffffu;
 constexpr int kMtRing = 1024;  // tempered-word ring (>= 624 + 16)
-constexpr int kMtMaxSub = 1 << kMtJumpLevels;
 
 __host__ __device__ inline uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
@@ -57,78 +53,13 @@ __host__ __device__ inline uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t m) {
   return m ^ (y >> 1) ^ ((0u - (y & 1u)) & kMtA);
 }
 
-// ------------------------------------------------------------------- host
-// A window (x_T .. x_T+623) as a ring: logical word j is w[(head + j) % 624].
-struct Ring {
-  uint32_t w[kMtN];
-  int head = 0;
-  void step() {  // -> (x_T+1 .. x_T+624)
-    const int h1 = head + 1 == kMtN ? 0 : head + 1;
-    const int hm = head + kMtM >= kMtN ? head + kMtM - kMtN : head + kMtM;
-    w[head] = mt_mix(w[head], w[h1], w[hm]);
-    head = h1;
-  }
-  void to_linear(uint32_t* out) const {
-    for (int j = 0; j < kMtN; ++j) out[j] = w[(head + j) % kMtN];
-  }
-};
-
-// out = g(f)(win): window jumped by J words, g = x^J mod P.  The low 31 bits
-// of out[0] are not determined (they never reach an output or the dynamics).
-// Horner over 8-bit chunks of g: r = f^8(r) ^ T[chunk], T[b] = sum_j b_j f^j(win)
-// (256 precomputed windows), so a 624-word XOR per 8 coefficients instead of
-// one per set coefficient.
-void xor_into(Ring& r, const uint32_t* lin) {  // r_logical[j] ^= lin[j]
-  const int n1 = kMtN - r.head;
-  uint32_t* a = r.w + r.head;
-  for (int j = 0; j < n1; ++j) a[j] ^= lin[j];
-  for (int j = 0; j < r.head; ++j) r.w[j] ^= lin[n1 + j];
-}
-
-void mt_jump(const uint32_t* win, const uint64_t* g, uint32_t* out) {
-  constexpr int kQ = 8;
-  std::vector<uint32_t> T(static_cast<size_t>(1 << kQ) * kMtN, 0u);
-  {
-    Ring p;
-    std::memcpy(p.w, win, sizeof(p.w));
-    for (int j = 0; j < kQ; ++j) {  // T[2^j + b] = f^j(win) ^ T[b]
-      uint32_t fj[kMtN];
-      p.to_linear(fj);
-      const int bit = 1 << j;
-      for (int b = 0; b < bit; ++b) {
-        uint32_t* d = T.data() + static_cast<size_t>(bit + b) * kMtN;
-        const uint32_t* src = T.data() + static_cast<size_t>(b) * kMtN;
-        for (int i = 0; i < kMtN; ++i) d[i] = src[i] ^ fj[i];
-      }
-      p.step();
-    }
-  }
-  Ring r;
-  std::memset(r.w, 0, sizeof(r.w));
-  int top = kMtPolyWords * 64 - 1;
-  while (top >= 0 && !((g[top >> 6] >> (top & 63)) & 1u)) --top;
-  for (int c = top / kQ; c >= 0; --c) {
-    for (int i = 0; i < kQ; ++i) r.step();
-    const int bit0 = c * kQ;
-    const uint32_t chunk = static_cast<uint32_t>((g[bit0 >> 6] >> (bit0 & 63)) & ((1u << kQ) - 1u));
-    if (chunk) xor_into(r, T.data() + static_cast<size_t>(chunk) * kMtN);
-  }
-  r.to_linear(out);
-}
-
-void mt_advance(const uint32_t* win, uint64_t steps, uint32_t* out) {
-  Ring r;
-  std::memcpy(r.w, win, sizeof(r.w));
-  for (uint64_t i = 0; i < steps; ++i) r.step();
-  r.to_linear(out);
-}
-
 // ----------------------------------------------------------------- device
 struct MtArgs {
   const uint32_t* windows;  // [subs][624]; window 0 = CPython's array at time B
   uint8_t* coeffs;          // tm1 tiled vectors
   uint32_t* flag;           // != 0: a draw was rejected
   uint64_t n_elem, ncoef, vb;
+  uint64_t L;               // words per substream
   uint32_t idx;             // CPython index: stream words 0..623-idx are temper(window0[idx..])
   int32_t tm1;
 };
@@ -147,7 +78,7 @@ __global__ void __launch_bounds__(64) mt_coeffs_kernel(const MtArgs a) {
   __shared__ uint32_t R[kMtRing];
   const uint32_t lane = threadIdx.x;
   const uint64_t sub = blockIdx.x;
-  const uint64_t lo = sub * kMtJumpL, hi = lo + kMtJumpL;
+  const uint64_t lo = sub * a.L, hi = lo + a.L;
   uint64_t k = (lo + 16) / 17;                                   // first coefficient starting here
   const uint64_t k_end = (hi + 16) / 17 < a.ncoef ? (hi + 16) / 17 : a.ncoef;
   if (k >= k_end) return;
@@ -229,68 +160,16 @@ __global__ void __launch_bounds__(64) mt_coeffs_kernel(const MtArgs a) {
   }
 }
 
-// Window 1 + d (time B + (1 + d) L - h) from window 1 by the binary
-// decomposition of d (jumps of 2^k L; beyond the table, repeated top jumps).
-void mt_window_from1(const uint32_t* w1, uint64_t d, uint32_t* out) {
-  std::vector<uint32_t> cur(w1, w1 + kMtN), nxt(kMtN);
-  for (int lev = 0; d; ++lev, d >>= 1) {
-    if (lev == kMtJumpLevels - 1) {  // the rest: d times 2^lev L
-      for (uint64_t r = 0; r < d; ++r) {
-        mt_jump(cur.data(), kMtJumpPolys[1 + lev], nxt.data());
-        cur.swap(nxt);
-      }
-      break;
-    }
-    if (d & 1u) {
-      mt_jump(cur.data(), kMtJumpPolys[1 + lev], nxt.data());
-      cur.swap(nxt);
-    }
-  }
-  std::memcpy(out, cur.data(), kMtN * sizeof(uint32_t));
-}
-
 uint64_t mt_subs(uint64_t ncoef) {
   const uint64_t words = 17 * ncoef;
-  return words ? (words + kMtJumpL - 1) / kMtJumpL : 0;
+  const uint64_t L = mt_jump_words();
+  return words ? (words + L - 1) / L : 0;
 }
 
 }  // namespace
 }  // namespace dn
 
 using namespace dn;
-
-// Stream words are numbered from CPython's current position: words
-// 0 .. h-1 (h = 624 - index) are the rest of the current array, word w >= h
-// is output w - h of the window at time B (the current array).  After W words
-// CPython holds the window at time B + 624 q (q = ceil((W - h) / 624)
-// twists) with index W - h - 624 (q - 1).
-extern "C" int dn_mt19937_skip(uint32_t* mt_state, int32_t* mt_index, uint64_t words) {
-  if (!mt_state || !mt_index) return set_error(DN_ERR_ARG, "dn_mt19937_skip: null pointer");
-  const int32_t idx = *mt_index;
-  if (idx < 0 || idx > kMtN) return set_error(DN_ERR_ARG, "dn_mt19937_skip: bad MT index");
-  const uint64_t h = static_cast<uint64_t>(kMtN - idx);
-  if (words <= h) {
-    *mt_index = idx + static_cast<int32_t>(words);
-    return DN_OK;
-  }
-  const uint64_t m_end = words - h, q = (m_end + kMtN - 1) / kMtN, tf = kMtN * q + h;
-  const uint64_t sig = (tf - 1) / kMtJumpL;
-  std::vector<uint32_t> w(kMtN), fin(kMtN);
-  uint64_t t_sig = h;
-  if (sig == 0) {
-    std::memcpy(w.data(), mt_state, kMtN * sizeof(uint32_t));
-  } else {
-    std::vector<uint32_t> adv(kMtN), w1(kMtN);
-    mt_advance(mt_state, static_cast<uint64_t>(idx), adv.data());
-    mt_jump(adv.data(), kMtJumpPolys[0], w1.data());
-    mt_window_from1(w1.data(), sig - 1, w.data());
-    t_sig = sig * kMtJumpL;
-  }
-  mt_advance(w.data(), tf - t_sig, fin.data());
-  std::memcpy(mt_state, fin.data(), kMtN * sizeof(uint32_t));
-  *mt_index = static_cast<int32_t>(m_end - kMtN * (q - 1));
-  return DN_OK;
-}
 
 extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
   const uint64_t subs = tm1 > 0 ? mt_subs(n_elem * static_cast<uint64_t>(tm1)) : 0;
@@ -308,42 +187,15 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
   if (ncoef == 0) return DN_OK;
   if (!coeffs || !scratch) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
   const uint64_t subs = mt_subs(ncoef);
-  if (subs > static_cast<uint64_t>(kMtMaxSub))
+  if (subs > mt_jump_max_subs())
     return set_error(DN_ERR_UNSUPPORTED, "dn_mt19937_draw_coeffs_device: %llu words exceed the jump table",
                      static_cast<unsigned long long>(17 * ncoef));
   if (scratch_bytes < dn_mt19937_device_scratch_bytes(n_elem, tm1))
     return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: scratch too small");
-  const uint64_t W = 17 * ncoef, h = static_cast<uint64_t>(kMtN - idx);
 
-  // substream windows: 0 = CPython's array (time B); 1 = time B + L - h;
-  // 1 + d (d >= 1) = window 1 + d - 2^k jumped by 2^k L, 2^k <= d < 2^(k+1)
+  // substream windows (host jump-ahead, host_mt_jump.cpp)
   std::vector<uint32_t> wins(subs * kMtN);
-  std::memcpy(wins.data(), mt_state, kMtN * sizeof(uint32_t));
-  if (subs > 1) {
-    std::vector<uint32_t> adv(kMtN);
-    mt_advance(mt_state, static_cast<uint64_t>(idx), adv.data());
-    mt_jump(adv.data(), kMtJumpPolys[0], wins.data() + kMtN);
-  }
-  unsigned hw = std::thread::hardware_concurrency();
-  const unsigned nthr = hw ? (hw < 16 ? hw : 16) : 1;
-  for (int lev = 0; (1ull << lev) < subs - 1 && subs > 2; ++lev) {
-    const uint64_t d0 = 1ull << lev, d1 = (2ull << lev) < subs - 1 ? (2ull << lev) : subs - 1;
-    const uint64_t cnt = d1 - d0;  // windows 1 + d for d in [d0, d1)
-    auto work = [&](unsigned t) {
-      for (uint64_t i = t; i < cnt; i += nthr) {
-        const uint64_t d = d0 + i;
-        mt_jump(wins.data() + (1 + d - d0) * kMtN, kMtJumpPolys[1 + lev], wins.data() + (1 + d) * kMtN);
-      }
-    };
-    if (cnt < 4 || nthr == 1) {
-      work(0);
-      for (unsigned t = 1; t < nthr; ++t) work(t);
-    } else {
-      std::vector<std::thread> th;
-      for (unsigned t = 0; t < nthr; ++t) th.emplace_back(work, t);
-      for (auto& x : th) x.join();
-    }
-  }
+  mt_build_windows(mt_state, idx, subs, wins.data());
 
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
@@ -352,7 +204,7 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
   hipError_t err = hipMemsetAsync(flag, 0, 4, s);
   if (err == hipSuccess) err = hipMemcpyAsync(dwin, wins.data(), wins.size() * 4, hipMemcpyHostToDevice, s);
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: %s", hipGetErrorString(err));
-  MtArgs a{dwin, static_cast<uint8_t*>(coeffs), flag, n_elem, ncoef, dn_m521_vec_bytes(n_elem),
+  MtArgs a{dwin, static_cast<uint8_t*>(coeffs), flag, n_elem, ncoef, dn_m521_vec_bytes(n_elem), mt_jump_words(),
            static_cast<uint32_t>(idx), tm1};
   hipLaunchKernelGGL(mt_coeffs_kernel, dim3(static_cast<uint32_t>(subs)), dim3(64), 0, s, a);
   err = hipGetLastError();
@@ -360,20 +212,8 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
 
   // final CPython state while the device works
   std::vector<uint32_t> fin(kMtN);
-  int32_t fidx;
-  if (W <= h) {
-    std::memcpy(fin.data(), mt_state, kMtN * 4);
-    fidx = idx + static_cast<int32_t>(W);
-  } else {
-    const uint64_t m_end = W - h, q = (m_end + kMtN - 1) / kMtN;  // q twists
-    // window at time B + 624 q from the last substream window strictly before it
-    const uint64_t tf = kMtN * q + h;  // (time - B) + h
-    uint64_t sig = (tf - 1) / kMtJumpL;
-    if (sig > subs - 1) sig = subs - 1;
-    const uint64_t t_sig = sig == 0 ? h : sig * kMtJumpL;  // (T_sig - B) + h
-    mt_advance(wins.data() + sig * kMtN, tf - t_sig, fin.data());
-    fidx = static_cast<int32_t>(m_end - kMtN * (q - 1));
-  }
+  int32_t fidx = 0;
+  mt_final_state(mt_state, idx, 17 * ncoef, wins.data(), subs, fin.data(), &fidx);
   uint32_t hflag = 0;
   err = hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, s);
   if (err == hipSuccess) err = hipStreamSynchronize(s);
