@@ -6,8 +6,8 @@ the contiguous, tile-aligned element range `shard_range(N, r, world)` and
 splits it locally.  Because the M521 layout is tiled (256 elements per
 16896-byte tile), a tile-aligned shard of a vector is a contiguous byte range
 of the full vector, so the one exchange step — every rank receiving every
-share vector — is a single all-gather of each rank's [n_shares, shard_bytes]
-block followed by a [world, S, B] -> [S, world*B] permute.
+share vector — is one all-gather per share row straight into that row of the
+full vectors.
 
 Semantically, handing share x to party x is an all-to-all; the all-gather
 (every rank gets all shares) is what BASELINE config 4 specifies and is
@@ -42,6 +42,12 @@ def allgather_share_blocks(local_block, n_total: int, group=None):
                  shard, padded to the common tile count)
     Returns uint8 [S, world * shard_bytes]; its first vec_bytes(n_total) bytes
     per row are the full tiled vectors (the rest is tile padding).
+
+    One all-gather per share row, straight into that row of the output: rank
+    r's shard lands at byte r * shard_bytes, which is where its tiles belong
+    in the full vector, so no permute copy follows and the output is the only
+    buffer (S calls of world * shard_bytes each — 9 x 4.4 GB at config 4 —
+    are far past the size where RCCL's per-call cost matters).
     """
     import torch
     import torch.distributed as dist
@@ -50,9 +56,11 @@ def allgather_share_blocks(local_block, n_total: int, group=None):
     S, B = local_block.shape
     if B != shard_tiles(n_total, world) * field.TILE_BYTES:
         raise ValueError("allgather_share_blocks: block is not padded to the common shard size")
-    gathered = torch.empty((world * S, B), dtype=local_block.dtype, device=local_block.device)
-    dist.all_gather_into_tensor(gathered, local_block.contiguous(), group=group)
-    return gathered.view(world, S, B).permute(1, 0, 2).reshape(S, world * B)
+    src = local_block.contiguous()
+    out = torch.empty((S, world * B), dtype=local_block.dtype, device=local_block.device)
+    for s in range(S):
+        dist.all_gather_into_tensor(out[s], src[s], group=group)
+    return out
 
 
 def draw_coeffs_sharded(ss, n_total: int, device=None, group=None):
