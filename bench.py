@@ -353,13 +353,29 @@ def rows_bench(dev, log2n: int) -> dict:
     want = py_mimc7.data_commitment(data[:256])
     cdt = time.perf_counter() - t0
     mulmods = (1 << 15) * 10 * 13 * 4 + 256 * 127 * 2 * 13 * 4  # x^7 = 4 Montgomery products per round
+    # the same at 2^20 rows: enough rows to fill the chip (throughput- rather than latency-bound)
+    big = drng.standard_normal((1 << 20, 10))
+    big[:, -1] = drng.integers(0, 2, 1 << 20)
+    bdev = torch.from_numpy(big).to(dev)
+    broots = mimc7.calc_data_commitment(bdev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        broots = mimc7.calc_data_commitment(bdev)
+    bm = (time.perf_counter() - t0) / 3 * 1e3
+    bwant = py_mimc7.data_commitment(big[:128])
+    big_row = {"ms": bm, "rows_per_s": (1 << 20) / (bm * 1e-3),
+               "mont_mul_per_s": ((1 << 20) * 10 * 13 * 4 + 8192 * 127 * 2 * 13 * 4) / (bm * 1e-3),
+               "oracle_prefix_equal": broots[:1] == bwant}
+    del bdev
     rows["mimc7_commitment"] = {"workload": "calc_data_commitment, 2^15 rows x 10 cols -> 256 roots",
                                 "ms": mm, "rows_per_s": (1 << 15) / (mm * 1e-3),
                                 "mont_mul_per_s": mulmods / (mm * 1e-3),
                                 "parallelism": "one lane per row (512 waves for 1024 SIMDs), then one wave per "
                                                "128-row Merkle block: latency-bound chains at this size",
                                 "oracle_prefix_equal": roots[:2] == want, "bound": "valu (BN254 Montgomery mul)",
-                                "cpu_python": {"rows_per_s": 256 / cdt, "sample": "256 rows, Python ints 1 thread"}}
+                                "cpu_python": {"rows_per_s": 256 / cdt, "sample": "256 rows, Python ints 1 thread"},
+                                "at_2e20_rows": big_row}
     rows["mask_masking"] = {
         "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
         "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
