@@ -37,8 +37,13 @@ PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 PEAK_VALU_GOPS = 256 * 4 * 32 * 2.4
 
 
+# ds_read_b32 with every CU streaming (MI355X_MICROARCH.md §LDS: ≈75 TB/s)
+PEAK_LDS_B32_GBPS = 75000.0
+
+
 def roof(bound: str, achieved: float, note: str) -> dict:
-    peak, unit = (PEAK_HBM_GBPS, "GB/s") if bound == "hbm" else (PEAK_VALU_GOPS, "Gop/s")
+    peak, unit = {"hbm": (PEAK_HBM_GBPS, "GB/s"), "lds": (PEAK_LDS_B32_GBPS, "GB/s")}.get(
+        bound, (PEAK_VALU_GOPS, "Gop/s"))
     return {"bound": bound, "achieved": achieved, "peak": peak, "unit": unit, "frac": achieved / peak,
             "per_unit": note}
 FE_BYTES = 66           # ceil(521 / 8): one field element in the tiled layout
@@ -196,6 +201,69 @@ def config5_bench(log2n: int, rounds: int = 2) -> dict:
     return out
 
 
+def envelope_row(recs, reps: int, s, e) -> dict:
+    """Share envelope (second half): one receiver's packed
+    records -> "0x" + hex(base64(nonce || AES-256-CTR)) = the ASCII of
+    serialize.bytes_to_hex(aes.encrypt(key, records)) (crypto/aes/aes.py:8-14,
+    runner/horizontal/commu.py:23-49) and back.  LDS roofline: 14 rounds x 16
+    T-table lookups (4 B, conflict-free ds_read_b32) per 16-byte block."""
+    import base64
+    import shutil
+    import subprocess
+
+    from delta_node.crypto import aes
+    from oracle import c_oracle
+
+    key, nonce = bytes(range(32)), bytes(range(16, 32))
+    n = recs.numel()
+    env = aes.encrypt_vec(key, recs, nonce=nonce, hex=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        env = aes.encrypt_vec(key, recs, nonce=nonce, hex=True)
+    e.record()
+    torch.cuda.synchronize()
+    enc_ms = s.elapsed_time(e) / reps
+    back = aes.decrypt_vec(key, env, hex=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        back = aes.decrypt_vec(key, env, hex=True)
+    e.record()
+    torch.cuda.synchronize()
+    dec_ms = s.elapsed_time(e) / reps
+    units = 4096  # the first 4096 thread units (196 KB) against the oracle
+    m = base64.b64decode(bytes.fromhex(bytes(env[2:2 + 128 * units].cpu().numpy()).decode()))
+    oracle_ok = m[:16] == nonce and m[16:] == c_oracle.aes_ctr(key, nonce, bytes(recs[:len(m) - 16].cpu().numpy()))
+    text_bytes = env.numel()
+    lds_bytes = (n + 15) // 16 * 14 * 16 * 4
+    row = {"workload": f"packed records of share x=3 ({n / 1e9:.2f} GB) <-> '0x' + hex(base64(nonce || AES-256-CTR)) "
+                       f"({text_bytes / 1e9:.2f} GB)",
+           "encrypt_ms": enc_ms, "decrypt_ms": dec_ms,
+           "encrypt_plaintext_GBps": n / (enc_ms * 1e-3) / 1e9, "decrypt_plaintext_GBps": n / (dec_ms * 1e-3) / 1e9,
+           "roofline_lds": roof("lds", lds_bytes / (enc_ms * 1e-3) / 1e9,
+                                "14 rounds x 16 Te lookups x 4 B per 16-byte block (encrypt)"),
+           "roofline_hbm": roof("hbm", (n + text_bytes) / (enc_ms * 1e-3) / 1e9,
+                                "record bytes in + 2.67 x text bytes out (encrypt)"),
+           "bound": "lds + valu (T-table AES-256; base64 and hex fused)",
+           "roundtrip_equal": bool(torch.equal(back, recs)), "oracle_prefix_equal": bool(oracle_ok)}
+    del env, back
+    if shutil.which("openssl"):
+        # the reference's stack on one core: OpenSSL AES-256-CTR (what `cryptography` wraps; its CLI
+        # here) + CPython base64.b64encode + bytes.hex, on a 2^26-byte sample of the same records
+        sample = bytes(recs[: 1 << 26].cpu().numpy())
+        t0 = time.perf_counter()
+        ct = subprocess.run(["openssl", "enc", "-aes-256-ctr", "-K", key.hex(), "-iv", nonce.hex(), "-nosalt"],
+                            input=sample, capture_output=True, check=True).stdout
+        text = "0x" + base64.b64encode(nonce + ct).hex()
+        dt = time.perf_counter() - t0
+        row["cpu_baseline"] = {"plaintext_GBps": len(sample) / dt / 1e9, "cores": 1, "kind": "port",
+                               "sample": "2^26 record bytes: openssl enc -aes-256-ctr (AES-NI) + base64.b64encode "
+                                         "+ bytes.hex, 1 core",
+                               "text_prefix_equal": text[:2 + 8 * 4096] == "0x" + base64.b64encode(m[:3 * 4096]).hex()}
+    return row
+
+
 def rows_bench(dev, log2n: int) -> dict:
     """SURVEY §8(f) rows measured beside the headline (device-resident inputs):
     mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
@@ -284,6 +352,8 @@ def rows_bench(dev, log2n: int) -> dict:
                                             "cores": 1, "kind": "port",
                                             "sample": "2^16 shares, _share_to_bytes / _bytes_to_share restated "
                                                       "(oracle/py_shamir.py), 1 core"}}
+    rows["share_envelope"] = envelope_row(packed[:total], reps, s, e)
+    del packed, vec
     # device-PRNG split (dn_m521_split_prng, SURVEY §8(d) config 2'): coefficients generated in-kernel
     from delta_node.crypto.shamir import _native as _nat
 

@@ -9,6 +9,9 @@ namespace dn {
 // Record a thread-local error message and return `code` (printf-style).
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// Compute units of the current device (cached per device; shamir_m521.hip).
+int device_cu_count();
+
 // MT19937 jump-ahead (host_mt_jump.cpp): substream length in words, the most
 // substreams the jump table covers, substream start windows and CPython's
 // final state after `words` outputs (wins may be null).

@@ -603,6 +603,8 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   return check_launch(name);
 }
 
+int device_cu_count() { return cu_count(); }
+
 }  // namespace dn
 
 using namespace dn;

@@ -22,11 +22,42 @@ def lib():
         L.oracle_reconstruct.argtypes = [vp, vp, i32, u64, vp]
         L.oracle_chacha_block.argtypes = [vp, u64, u64, i32, vp]
         L.oracle_prng_coeffs.argtypes = [vp, u64, i32, u64, u64, i32, vp]
+        cp = ctypes.c_char_p
+        L.oracle_aes_sbox.argtypes = [ctypes.c_uint8]
+        L.oracle_aes_sbox.restype = ctypes.c_uint8
+        L.oracle_aes_expand.argtypes = [cp, i32, vp]
+        L.oracle_aes_expand.restype = i32
+        L.oracle_aes_block.argtypes = [cp, i32, cp, vp]
+        L.oracle_aes_ctr.argtypes = [cp, i32, cp, cp, vp, u64]
         for f in (L.oracle_draw_coeffs, L.oracle_mt_words, L.oracle_split, L.oracle_reconstruct,
-                  L.oracle_chacha_block, L.oracle_prng_coeffs):
+                  L.oracle_chacha_block, L.oracle_prng_coeffs, L.oracle_aes_block, L.oracle_aes_ctr):
             f.restype = None
         _lib = L
     return _lib
+
+
+def aes_sbox(x: int) -> int:
+    return int(lib().oracle_aes_sbox(x))
+
+
+def aes_expand(key: bytes) -> bytes:
+    """FIPS-197 round keys, 16 (rounds + 1) bytes."""
+    buf = ctypes.create_string_buffer(240)
+    nr = lib().oracle_aes_expand(key, len(key), buf)
+    return buf.raw[: 16 * (nr + 1)]
+
+
+def aes_block(key: bytes, block: bytes) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().oracle_aes_block(key, len(key), block, out)
+    return out.raw
+
+
+def aes_ctr(key: bytes, iv: bytes, data: bytes) -> bytes:
+    """data XOR the AES-CTR keystream of (key, iv): 128-bit big-endian counter."""
+    out = ctypes.create_string_buffer(max(1, len(data)))
+    lib().oracle_aes_ctr(key, len(key), iv, bytes(data), out, len(data))
+    return out.raw[: len(data)]
 
 
 def draw_coeffs(seed: int, n: int, tm1: int) -> np.ndarray:

@@ -33,6 +33,7 @@ def header_symbols():
 
 
 def test_library_exports_header_symbols():
+    from delta_node.crypto import aes
     from delta_node.crypto.shamir import codec
     from delta_node.utils import _mask_native, mimc7
 
@@ -41,7 +42,7 @@ def test_library_exports_header_symbols():
     L = _native.lib()
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
-    assert sorted(_native.EXPORTS + _mask_native.EXPORTS + codec.EXPORTS + mimc7.EXPORTS) == syms
+    assert sorted(_native.EXPORTS + _mask_native.EXPORTS + codec.EXPORTS + mimc7.EXPORTS + aes.EXPORTS) == syms
 
 
 def test_version_and_sizes():
