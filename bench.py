@@ -64,10 +64,17 @@ def cpu_baseline(t: int, n: int, xs, budget_s: float, procs: int = 16) -> dict:
     from oracle.py_shamir import time_elements, time_elements_star
 
     half = budget_s / 2
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     done, dt = time_elements(t, n, xs, half, seed=7)
     out = {"value": done / dt, "unit": "elements/s", "cores": 1, "kind": "port",
            "sample": f"{done} elements x (make_shares t={t} n={n} + resolve_shares xs={list(xs)}), "
-                     f"pure-Python restatement of delta_node/crypto/shamir, {dt:.1f} s on 1 core"}
+                     f"pure-Python restatement of delta_node/crypto/shamir, {dt:.1f} s on 1 core",
+           "cpu_model": cpu_model, "host_cpus": os.cpu_count()}
     try:
         with mp.get_context("spawn").Pool(procs) as pool:
             res = pool.map(time_elements_star, [(t, n, list(xs), half, 100 + i) for i in range(procs)])
