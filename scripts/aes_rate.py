@@ -2,7 +2,7 @@
 """Share-envelope kernel rates on one GPU: AES-256-CTR,
 encrypt to base64 / to "0x"+hex and back, over a message the size of one
 share's packed records at 2^24 elements (1.13 GB), for both LDS table layouts
-(DN_AES_TABLES=4 / 2).  HIP events on the launch stream; one JSON line per case.
+(DN_AES_TABLES=4 / 2) and store policies (DN_AES_STORE).  HIP events on the launch stream; one JSON line per case.
 """
 import json
 import os
