@@ -11,6 +11,10 @@ Runner side (this process), for a masked result {'w': {'w': int64[N]}}:
   encode  each share vector -> the reference's `_share_to_bytes` records
           (shamir.py:28-33) on the GPU, plus a uint8 record-length vector
   D2H     records + lengths into pinned host buffers
+  seal    (--seal) each share's body sealed for its receiver as the reference
+          sends shares: "0x" + hex(base64(nonce || AES-256-CTR(key, body)))
+          (crypto/aes/aes.py:8-14 + serialize.bytes_to_hex,
+          runner/horizontal/commu.py:23-49), on the GPU
   HTTP    one POST per share x to the peer (octet-stream), each share on its
           own keep-alive connection and sender thread, overlapped with the
           next share's encode + D2H
@@ -86,7 +90,8 @@ class _Peer(http.server.BaseHTTPRequestHandler):
         if self.path.startswith("/secret_shares/"):
             x = int(self.path.rsplit("/", 1)[1])
             body = self._body(slot=x)
-            self.store[x] = (body, int(self.headers["X-Records-Bytes"]), int(self.headers["X-Elements"]))
+            self.store[x] = (body, int(self.headers["X-Records-Bytes"]), int(self.headers["X-Elements"]),
+                             self.headers.get("X-Sealed") == "1")
             return self._reply({"x": x, "bytes": len(body)})
         if self.path == "/verify":
             req = json.loads(bytes(self._body()))
@@ -104,16 +109,20 @@ def _verify(store: dict, req: dict) -> dict:
     import torch
     import xxhash
 
-    from delta_node.crypto import shamir
+    from delta_node.crypto import aes, shamir
     from delta_node.crypto.shamir import codec
 
     n, xs, t = int(req["n"]), [int(x) for x in req["xs"]], int(req["t"])
+    keys = [bytes.fromhex(k) for k in req.get("keys", [])]
     dev = torch.device("cuda", 0)
     vecs = []
     for x in xs:
-        body, rec_bytes, n_el = store[x]
+        body, rec_bytes, n_el, sealed = store[x]
         assert n_el == n
-        raw = torch.from_numpy(body)
+        if sealed:  # the receiver's side: hex_to_bytes + aes.decrypt (runner/horizontal/agg.py:258-266)
+            raw = aes.decrypt_vec(keys[x - 1], torch.from_numpy(body).to(dev), hex=True)
+        else:
+            raw = torch.from_numpy(body)
         packed = raw[:rec_bytes].to(dev)
         lens = raw[rec_bytes:rec_bytes + n].to(dev).to(torch.int64)
         offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
@@ -160,14 +169,15 @@ def _post(conn: http.client.HTTPConnection, path: str, body, headers=None) -> di
 
 
 def run_round(n_elem: int, port: int, t: int = 3, n_shares: int = 5, coeffs: str = "prng",
-              verify_xs=(1, 3, 5), seed: int = 0) -> dict:
-    """One timed round; returns the stage timings and the peer's verification."""
+              verify_xs=(1, 3, 5), seed: int = 0, seal: bool = False) -> dict:
+    """One timed round; returns the stage timings and the peer's verification.
+    seal: each body goes out as the receiver's AES envelope in JSON form."""
     import cloudpickle
     import numpy as np
     import torch
     import xxhash
 
-    from delta_node.crypto import shamir
+    from delta_node.crypto import aes, shamir
     from delta_node.crypto.shamir import codec
 
     dev = torch.device("cuda", 0)
@@ -179,7 +189,11 @@ def run_round(n_elem: int, port: int, t: int = 3, n_shares: int = 5, coeffs: str
     # pinned staging, allocated once per runner (untimed)
     sec_pin = torch.empty(n_elem, dtype=torch.int64, pin_memory=True)
     cap = int(codec._lib().dn_m521_encoded_capacity(n_elem, n_shares))
-    stage = [torch.empty(cap + n_elem, dtype=torch.uint8, pin_memory=True) for _ in range(n_shares)]
+    body_cap = cap + n_elem
+    if seal:  # "0x" + hex(base64(nonce || body)); per-receiver keys (the runner's ECDH keys in the reference)
+        body_cap = 2 + int(aes.aes._lib().dn_aes_encrypt_len(cap + n_elem, 1))
+        keys = [np.random.default_rng([seed, x]).bytes(32) for x in range(1, n_shares + 1)]
+    stage = [torch.empty(body_cap, dtype=torch.uint8, pin_memory=True) for _ in range(n_shares)]
     copy_stream = torch.cuda.Stream()
     conns = [http.client.HTTPConnection("127.0.0.1", port, timeout=600) for _ in range(n_shares)]
     pool = ThreadPoolExecutor(n_shares)
@@ -211,15 +225,24 @@ def run_round(n_elem: int, port: int, t: int = 3, n_shares: int = 5, coeffs: str
         recs, offs = codec.encode_share_vec(shares[x - 1], n_elem, x)
         lens = (offs[1:] - offs[:-1]).to(torch.uint8)
         nb = recs.numel()
+        if seal:
+            plain = torch.empty(nb + n_elem, dtype=torch.uint8, device=dev)
+            plain[:nb].copy_(recs)
+            plain[nb:].copy_(lens)
+            text = aes.encrypt_vec(keys[x - 1], plain, hex=True)
+            parts, size = [(0, text)], text.numel()
+        else:
+            parts, size = [(0, recs), (nb, lens)], nb + n_elem
         with torch.cuda.stream(copy_stream):
             copy_stream.wait_stream(torch.cuda.current_stream())
-            buf[:nb].copy_(recs, non_blocking=True)
-            buf[nb:nb + n_elem].copy_(lens, non_blocking=True)
+            for off, part in parts:
+                buf[off:off + part.numel()].copy_(part, non_blocking=True)
         copy_stream.synchronize()
         enc_s += time.perf_counter() - te
-        body = memoryview(buf.numpy())[: nb + n_elem]
+        body = memoryview(buf.numpy())[:size]
         pending.append(pool.submit(_post, conns[x - 1], f"/secret_shares/{x}", body,
-                                   {"X-Records-Bytes": str(nb), "X-Elements": str(n_elem)}))
+                                   {"X-Records-Bytes": str(nb), "X-Elements": str(n_elem),
+                                    "X-Sealed": "1" if seal else "0"}))
     replies = [p.result() for p in pending]
     wall = time.perf_counter() - t0
     st["encode_d2h_s"] = enc_s
@@ -231,7 +254,10 @@ def run_round(n_elem: int, port: int, t: int = 3, n_shares: int = 5, coeffs: str
     st["elems_per_s"] = n_elem / wall
     st["http_GBps"] = st["bytes_posted"] / wall / 1e9
     digest = xxhash.xxh64(src.view(np.uint8)).hexdigest()
-    ver = _post(conns[0], "/verify", json.dumps({"n": n_elem, "xs": list(verify_xs), "t": t, "digest": digest}).encode())
+    req = {"n": n_elem, "xs": list(verify_xs), "t": t, "digest": digest}
+    if seal:
+        req["keys"] = [k.hex() for k in keys]
+    ver = _post(conns[0], "/verify", json.dumps(req).encode())
     st["peer_verified"] = bool(ver.get("ok"))
     for c in conns:
         c.close()
@@ -264,6 +290,7 @@ def main() -> int:
     ap.add_argument("--port", type=int, default=18931)
     ap.add_argument("--coeffs", choices=("prng", "mt"), default="prng")
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--seal", action="store_true", help="send each body as the receiver's AES envelope (JSON form)")
     args = ap.parse_args()
     if args.serve:
         serve(args.serve)
@@ -271,11 +298,11 @@ def main() -> int:
     proc = start_peer(args.port)
     try:
         _wait_ready(args.port)
-        run_round(1 << 12, args.port, coeffs=args.coeffs)  # warm-up: contexts, kernels, connection path
+        run_round(1 << 12, args.port, coeffs=args.coeffs, seal=args.seal)  # warm-up: contexts, kernels, connections
         ok = True
         for r in range(args.rounds):
-            st = run_round(1 << args.log2n, args.port, coeffs=args.coeffs, seed=r + 1)
-            st.update({"round": r, "N": 1 << args.log2n, "t": 3, "n": 5, "coeffs": args.coeffs})
+            st = run_round(1 << args.log2n, args.port, coeffs=args.coeffs, seed=r + 1, seal=args.seal)
+            st.update({"round": r, "N": 1 << args.log2n, "t": 3, "n": 5, "coeffs": args.coeffs, "sealed": args.seal})
             print(json.dumps(st), flush=True)
             ok = ok and st["peer_verified"]
     finally:

@@ -18,15 +18,17 @@ def _e2e():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("coeffs", ["prng", "mt"])
-def test_masked_result_round_over_loopback(coeffs):
+@pytest.mark.parametrize("coeffs,seal", [("prng", False), ("mt", False), ("prng", True)])
+def test_masked_result_round_over_loopback(coeffs, seal):
+    """seal: every body travels as the receiver's AES envelope in JSON form
+    ("0x" + hex(base64(nonce || AES-256-CTR))) and the peer opens it on its GPU."""
     e2e = _e2e()
-    port = 18000 + os.getpid() % 1000 + (0 if coeffs == "prng" else 1000)
+    port = 18000 + os.getpid() % 1000 + (0 if coeffs == "prng" else 1000) + (2000 if seal else 0)
     proc = e2e.start_peer(port)
     try:
         e2e._wait_ready(port)
-        st = e2e.run_round((1 << 14) + 77, port, coeffs=coeffs, seed=5)
+        st = e2e.run_round((1 << 14) + 77, port, coeffs=coeffs, seed=5, seal=seal)
     finally:
         e2e.stop_peer(proc, port)
     assert st["peer_verified"]
-    assert st["bytes_posted"] > 5 * 66 * (1 << 14)
+    assert st["bytes_posted"] > 5 * 66 * (1 << 14) * (2.6 if seal else 1)
