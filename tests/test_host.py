@@ -184,6 +184,10 @@ def test_serialize_and_op_mirror():
     for v in (0, 1, 255, 256, P, 2**64 - 1):
         assert serialize.int_to_bytes(v) == v.to_bytes((v.bit_length() + 7) // 8, "big")
         assert serialize.bytes_to_int(serialize.int_to_bytes(v)) == v
+    # the reference's own cases (tests/serialize/hex_test.py:3-7)
+    assert serialize.bytes_to_hex(bytes([255])) == "0xff"
+    assert serialize.bytes_to_hex(bytes([255]), with0x=False) == "ff"
+    assert serialize.bytes_to_hex(bytes([255]), length=2) == "0x00ff"
     assert serialize.bytes_to_hex(b"\x01\x02", length=4) == "0x00000102"
     assert serialize.hex_to_bytes("0x0102", length=3) == b"\x00\x01\x02"
     assert op.inverse_mod(3, P) * 3 % P == 1
