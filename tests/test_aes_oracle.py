@@ -98,3 +98,24 @@ def test_no_cpu_cipher():
         pytest.skip("a HIP device is visible")
     with pytest.raises(RuntimeError, match="no HIP device"):
         aes.encrypt(bytes(32), b"data")
+
+
+def test_c_abi_argument_errors_before_any_device_work():
+    """The C-ABI's host-side checks (dn_aes.h): they return before touching a
+    device pointer, so fake pointers are safe here."""
+    from delta_node.crypto.shamir import _native
+
+    L = aes_mod._lib()
+    key, iv = bytes(range(32)), bytes(16)
+    assert L.dn_aes_encrypt(key, 20, iv, 16, 32, 4096, 0, None) == _native.DN_ERR_ARG
+    assert "Invalid key size (160) for AES." in _native.last_error()
+    assert L.dn_aes_encrypt(key, 32, iv, 16, 32, 4097, 1, None) == _native.DN_ERR_ARG  # misaligned output
+    assert "16-byte aligned" in _native.last_error()
+    assert L.dn_aes_encrypt(key, 32, None, 16, 32, 4096, 0, None) == _native.DN_ERR_ARG
+    assert L.dn_aes_encrypt(key, 32, iv, None, 32, 4096, 0, None) == _native.DN_ERR_ARG
+    assert L.dn_aes_ctr(key, 32, None, 16, 4096, 64, None) == _native.DN_ERR_ARG
+    assert L.dn_aes_ctr(key, 32, iv, 16, 4096, 0, None) == _native.DN_OK  # nothing to do
+    assert L.dn_aes_decrypt(key, 32, 16, 23, 0, 4096, 64, 8, 8, None) == _native.DN_ERR_RETRY  # < a nonce
+    assert L.dn_aes_decrypt(key, 32, 16, 49, 1, 4096, 64, 8, 8, None) == _native.DN_ERR_RETRY  # odd hex
+    assert L.dn_aes_decrypt(key, 32, 16, 64, 0, 4096, 1, 8, 8, None) == _native.DN_ERR_ARG  # capacity 1 < 32
+    assert L.dn_aes_decrypt(key, 16, 16, 64, 0, None, 64, 8, 8, None) == _native.DN_ERR_ARG  # null output
