@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Headline benchmark: device-resident Shamir 3-of-5 split + reconstruct over
-GF(2^521 - 1), 2^24 int64 elements per GPU (BASELINE.json `metric`, configs 2+3).
+GF(2^521 - 1) of one 2^24-element int64 vector (BASELINE.json `metric`, configs 2+3).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -8,8 +8,10 @@ GF(2^521 - 1), 2^24 int64 elements per GPU (BASELINE.json `metric`, configs 2+3)
 One step = `dn_m521_split_u64` (t=3, n=5) over the rank's N elements, then
 `dn_m521_reconstruct` of shares xs (default 1,3,5) back to int64, inputs
 resident in HBM before the timed region (secrets + MT19937 coefficients drawn
-exactly as the reference's `make_shares` would draw them).  Weak scaling: each
-rank owns N elements; value = all ranks' elements / max-over-ranks time.
+exactly as the reference's `make_shares` would draw them).  Strong scaling, as
+the metric names it: ONE 2^24-element vector, rank r splitting its tile-aligned
+shard (dist.shard_range); value = 2^24 / max-over-ranks time per step.  At
+N > 1 the line also carries `weak_scaling` (2^24 elements per GPU).
 
 Prints ONE JSON line (rank 0) with `roofline` for the dominant kernel (split;
 its average launch time from HIP events on the launch stream, algorithmic
@@ -85,6 +87,50 @@ def cpu_baseline(t: int, n: int, xs, budget_s: float, procs: int = 16) -> dict:
     return out
 
 
+def measure_ceiling(dev, sec, coeffs, shares, N: int, t: int, n: int, reps: int = 5) -> dict:
+    """Same-buffer HBM ceiling of the split (lib/libdn_diag.so,
+    dn_diag_tile_stream): the split's exact bytes per tile — the rank's
+    secrets, t-1 coefficient rows read, n share rows written — over the SAME
+    buffers (so the same physical pages, whose placement sets this part's
+    write rate: DESIGN.md §5.1), with 16-B non-temporal accesses and no
+    arithmetic; the fastest of four grid sizes.  Overwrites `shares`."""
+    import ctypes
+
+    from delta_node.crypto.shamir import field
+
+    diag = ctypes.CDLL(os.path.join(ROOT, "delta-node_amd", "lib", "libdn_diag.so"))
+    vp = ctypes.c_void_p
+    if N % field.TILE:
+        return None
+    ins = (vp * 8)(sec.data_ptr(), *[coeffs[j].data_ptr() for j in range(t - 1)])
+    ibpt = (ctypes.c_uint32 * 8)(8 * field.TILE, *([field.TILE_BYTES] * (t - 1)))
+    outs = (vp * 16)(*[shares[x].data_ptr() for x in range(n)])
+    obpt = (ctypes.c_uint32 * 16)(*([field.TILE_BYTES] * n))
+    stream = torch.cuda.current_stream()
+
+    def launch(grid):
+        rc = diag.dn_diag_tile_stream(ins, ibpt, t, outs, obpt, n, ctypes.c_uint64(N // field.TILE), grid,
+                                      vp(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"dn_diag_tile_stream rc={rc}")
+
+    best = None
+    for grid in (256, 1024, 4096, 16384):
+        launch(grid)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        for _ in range(reps):
+            launch(grid)
+        e.record(stream)
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / reps
+        if best is None or ms < best["ms"]:
+            best = {"ms": ms, "grid": grid}
+    best["kernel"] = ("dn_diag_tile_stream: the split's bytes over the same buffers, 16-B nt loads then stores "
+                      "per tile, no arithmetic (fastest of grids 256/1024/4096/16384)")
+    return best
+
+
 def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int = 5) -> dict:
     """BASELINE config 4: 5-of-9 split of a 2^26-element vector sharded by
     element across the ranks (rank r: `dist.shard_range`), then one RCCL
@@ -145,7 +191,8 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
     if world > 1:
         import torch.distributed as tdist
 
-        tt = torch.tensor([split_ms], dtype=torch.float64, device=dev)
+        cdev = dev if tdist.get_backend() == "nccl" else torch.device("cpu")
+        tt = torch.tensor([split_ms], dtype=torch.float64, device=cdev)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         split_max_ms = float(tt.item())
         full = sdist.allgather_share_blocks(block, N_total)  # warm-up (RCCL channels)
@@ -160,12 +207,16 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
         gdt = (time.perf_counter() - g0) / 3
         same = bool(torch.equal(full[:, rank * B: rank * B + vb], block[:, :vb]))
         del full
-        flags = torch.tensor([int(ok and same)], dtype=torch.int32, device=dev)
+        flags = torch.tensor([int(ok and same)], dtype=torch.int32, device=cdev)
         tdist.all_reduce(flags, op=tdist.ReduceOp.MIN)
         recv = block.numel() * (world - 1)
         out["allgather"] = {"ms": gdt * 1e3, "bytes_received_per_gpu": recv, "GBps_per_gpu": recv / gdt / 1e9,
                             "blocks_equal": same, "all_ranks_ok": bool(flags.item())}
     out["split_elems_per_s_aggregate"] = N_total / (split_max_ms * 1e-3)
+    ceil = measure_ceiling(dev, sec, coeffs, shares, nl, t, n)
+    if ceil:
+        out["roofline"]["ceiling_measured"] = {**ceil, "GBps": nl * per_elem / (ceil["ms"] * 1e-3) / 1e9,
+                                               "split_frac_of_ceiling": ceil["ms"] / split_ms}
     del block, shares, coeffs, sec, rec
     torch.cuda.empty_cache()
     return out
@@ -481,7 +532,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log2n", type=int, default=24, help="elements per GPU = 2^log2n")
+    ap.add_argument("--log2n", type=int, default=24, help="elements of the vector = 2^log2n (sharded over the ranks)")
     ap.add_argument("--t", type=int, default=3)
     ap.add_argument("--shares", type=int, default=5)
     ap.add_argument("--xs", type=str, default="1,3,5")
@@ -513,27 +564,44 @@ def main():
         else:
             dist.init_process_group(backend)
     dev = torch.device("cuda", torch.cuda.current_device())
+    # small control-plane tensors (timings, parity flags): device under nccl, host under gloo
+    cdev = dev if world == 1 or torch.distributed.get_backend() == "nccl" else torch.device("cpu")
 
     from delta_node.crypto import shamir
     from delta_node.crypto.shamir import _native, field
+    from delta_node.crypto.shamir import dist as sdist
 
-    N = 1 << args.log2n
+    N_total = 1 << args.log2n
     t, n = args.t, args.shares
     xs = [int(x) for x in args.xs.split(",")]
+    # Strong scaling (BASELINE metric: ONE 2^24 vector): rank r
+    # owns the tile-aligned range shard_range(N_total, r, world) of it.
+    lo, hi = sdist.shard_range(N_total, rank, world) if world > 1 else (0, N_total)
+    N = hi - lo
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
 
     # ---- inputs resident in HBM (untimed) ---------------------------------
+    # secrets: one synthetic vector; coefficients: the reference's MT19937
+    # stream for the WHOLE vector (N make_shares calls on one instance), each
+    # rank drawing only its shard on its GPU (dist.draw_coeffs_sharded)
     ss = shamir.SecretShare(t)
-    ss.random.seed(1 + rank)
-    sec_h = secrets_int64(1 + rank, N)
+    ss.random.seed(1)
+    sec_h = secrets_int64(1, N_total)[lo:hi].copy()
     sec = torch.from_numpy(sec_h).to(dev)
-    coeffs = ss.draw_coeffs_vec(N, dev)  # MT19937, as N make_shares calls would draw
     vb = field.vec_bytes(N)
+    if world > 1:
+        coeffs = sdist.draw_coeffs_sharded(ss, N_total, dev)[:, :vb].contiguous()
+    else:
+        coeffs = ss.draw_coeffs_vec(N_total, dev)
     shares = torch.empty((n, vb), dtype=torch.uint8, device=dev)
     rec = torch.empty(N, dtype=torch.int64, device=dev)
     w = _native.lagrange(xs, t)
     share_rows = [shares[x - 1] for x in xs]
     torch.cuda.synchronize()
-
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
@@ -546,31 +614,30 @@ def main():
         if ev:
             ev[2].record(stream)
 
-    def barrier():
+    def timed_steps(fn, steps):
+        for _ in range(args.warmup):
+            fn()
+        barrier()
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(evs[i])
+        barrier()
+        el = time.perf_counter() - t0
         if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
+            tt = torch.tensor([el], dtype=torch.float64, device=cdev)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, evs
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, evs = timed_steps(step, args.steps)
     split_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     recon_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
     # ---- parity of what was timed (cheap, size-independent + sampled) -----
     roundtrip = bool(torch.equal(rec, sec))
-    sample = 2048
+    sample = min(2048, N)
     from oracle import c_oracle
 
     co_h = np.stack([field.vec_to_limbs(coeffs[j, : field.vec_bytes(sample)].cpu().numpy(), sample)
@@ -578,29 +645,59 @@ def main():
     want = c_oracle.split(sec_h[:sample], co_h, t, n)
     got = np.stack([field.vec_to_limbs(shares[x, : field.vec_bytes(sample)].cpu().numpy(), sample) for x in range(n)])
     oracle_ok = bool(np.array_equal(got, want))
+    all_ok = roundtrip and oracle_ok
+    if world > 1:  # every rank's parity, not only rank 0's
+        fl = torch.tensor([int(all_ok)], dtype=torch.int32, device=cdev)
+        torch.distributed.all_reduce(fl, op=torch.distributed.ReduceOp.MIN)
+        all_ok = bool(fl.item())
+
+    # ---- same-buffer ceiling: the split's bytes through the same pages -----
+    ceiling = measure_ceiling(dev, sec, coeffs, shares, N, t, n) if N >= (1 << 20) else None
+
+    # ---- N > 1: the weak-scaling figure (2^log2n elements per GPU) --------
+    weak = None
+    if world > 1:
+        del shares, coeffs, share_rows, rec, sec
+        torch.cuda.empty_cache()
+        ssw = shamir.SecretShare(t)
+        ssw.random.seed(1 + rank)
+        wsec = torch.from_numpy(secrets_int64(1 + rank, N_total)).to(dev)
+        wco = ssw.draw_coeffs_vec(N_total, dev)
+        wsh = torch.empty((n, field.vec_bytes(N_total)), dtype=torch.uint8, device=dev)
+        wrec = torch.empty(N_total, dtype=torch.int64, device=dev)
+        wrows = [wsh[x - 1] for x in xs]
+
+        def wstep(ev=None):
+            _native.split_u64(wsec, wco, wsh, N_total, t, n)
+            _native.reconstruct(wrows, w, out_u64=wrec, n=N_total)
+
+        wel, _ = timed_steps(wstep, args.steps)
+        wok = torch.tensor([int(torch.equal(wrec, wsec))], dtype=torch.int32, device=cdev)
+        torch.distributed.all_reduce(wok, op=torch.distributed.ReduceOp.MIN)
+        weak = {"value": N_total * world * args.steps / wel, "unit": "elements/s", "elements_per_gpu": N_total,
+                "ms_per_step": wel / args.steps * 1e3, "scaling": "weak", "roundtrip_all_ranks": bool(wok.item())}
+        del wsec, wco, wsh, wrec, wrows
+        torch.cuda.empty_cache()
 
     # ---- optional: RCCL all-gather of share blocks (reported separately) --
     allgather = None
     if args.allgather and world > 1:
-        from delta_node.crypto.shamir import dist as sdist
-
-        block = shares  # every rank holds N elements: equal tile-aligned shards
+        shb = torch.zeros((n, sdist.shard_tiles(N_total, world) * field.TILE_BYTES), dtype=torch.uint8, device=dev)
         for _ in range(2):
-            sdist.allgather_share_blocks(block, N * world)
+            sdist.allgather_share_blocks(shb, N_total)
         barrier()
         g0 = time.perf_counter()
         reps = 3
         for _ in range(reps):
-            full = sdist.allgather_share_blocks(block, N * world)
+            full = sdist.allgather_share_blocks(shb, N_total)
         barrier()
         gdt = (time.perf_counter() - g0) / reps
-        recv = block.numel() * (world - 1)
+        recv = shb.numel() * (world - 1)
         allgather = {"ms": gdt * 1e3, "bytes_received_per_gpu": recv, "GBps_per_gpu": recv / gdt / 1e9}
-        del full
+        del full, shb
 
     # ---- report -------------------------------------------------------------
-    total_elems = N * world * args.steps
-    value = total_elems / elapsed
+    value = N_total * args.steps / elapsed
     split_bytes = N * (8 + (t - 1) * FE_BYTES + n * FE_BYTES)
     recon_bytes = N * (len(xs) * FE_BYTES + 8)
     achieved = split_bytes / (split_ms * 1e-3) / 1e9
@@ -614,12 +711,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic int64 secrets (numpy PCG64) + MT19937 coefficients drawn as make_shares draws them",
-        "config": {"workload": f"{t}-of-{n} split + reconstruct(xs={xs}) of 2^{args.log2n} int64 elements per GPU, "
-                               f"GF(2^521-1)", "elements_per_gpu": N, "threshold": t, "shares": n, "xs": xs,
+        "config": {"workload": f"{t}-of-{n} split + reconstruct(xs={xs}) of one 2^{args.log2n}-element int64 "
+                               f"vector, GF(2^521-1), sharded by element over {world} GPU(s)",
+                   "elements_total": N_total, "elements_per_gpu": N, "threshold": t, "shares": n, "xs": xs,
                    "parallelism": f"element-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS,
@@ -628,19 +726,26 @@ def main():
                                  if abs((traffic or {}).get("split_bytes_per_launch", 0) - split_bytes)
                                  < 0.01 * split_bytes else None),
                      "kernel": "dn::split_kernel<3, false, false, false, 2>",
-                     "algorithmic_bytes_per_launch": split_bytes, "avg_launch_ms": split_ms},
+                     "algorithmic_bytes_per_launch": split_bytes, "avg_launch_ms": split_ms,
+                     "ceiling_measured": ceiling and {
+                         **ceiling, "GBps": split_bytes / (ceiling["ms"] * 1e-3) / 1e9,
+                         "split_frac_of_ceiling": ceiling["ms"] / split_ms}},
         "kernels": {"split_ms": split_ms, "reconstruct_ms": recon_ms,
                     "split_GBps": achieved, "reconstruct_GBps": recon_bytes / (recon_ms * 1e-3) / 1e9,
                     "split_elems_per_s": N / (split_ms * 1e-3), "reconstruct_elems_per_s": N / (recon_ms * 1e-3)},
-        "parity": {"roundtrip_equal": roundtrip, "c_oracle_sample_equal": oracle_ok, "sample": sample},
+        "parity": {"roundtrip_equal": roundtrip, "c_oracle_sample_equal": oracle_ok, "sample": sample,
+                   "all_ranks_ok": all_ok},
     }
+    if weak:
+        line["weak_scaling"] = weak
     if allgather:
         line["allgather"] = allgather
     if args.config4:
-        del shares, coeffs, share_rows
+        if world == 1:
+            del shares, coeffs, share_rows
         torch.cuda.empty_cache()
         line["config4"] = config4_bench(dev, world, rank, args.config4_log2n)
-    if args.rows:
+    if args.rows and world == 1:
         line["rows"] = rows_bench(dev, args.log2n)
     if args.config5 and world == 1:
         line["config5"] = config5_bench(args.log2n)
@@ -650,7 +755,7 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
-    if not (roundtrip and oracle_ok):
+    if not all_ok:
         sys.exit(3)
 
 

@@ -591,7 +591,7 @@ static int expand_key(const uint8_t* key, int key_bytes, uint32_t rk[60], int* n
 
 // DN_AES_TABLES=2 selects the 64-KB two-table layout for AES-256 (A/B hook, read per call).
 static int aes_tables() {
-  const char* e = std::getenv("DN_AES_TABLES");
+  const char* e = tune_env("DN_AES_TABLES");
   return (e && e[0] == '2') ? 2 : 4;
 }
 
@@ -691,7 +691,7 @@ extern "C" int dn_aes_encrypt(const uint8_t* key, int key_bytes, const uint8_t* 
   set_iv(a, nonce);
   a.n = n;
   a.units = (n + 16 + 47) / 48;
-  const char* st = std::getenv("DN_AES_STORE");
+  const char* st = tune_env("DN_AES_STORE");
   a.plain = (st && st[0] == 'n') ? 0u : 1u;  // plain vs nt: within a few % either way (profiles/r01/aes/)
   return dispatch(nr, kEncrypt, hex != 0, a.units, stream, a, "dn_aes_encrypt");
 }

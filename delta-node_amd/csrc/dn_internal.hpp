@@ -2,10 +2,25 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "dn_shamir.h"
 
 namespace dn {
+// A/B tuning knobs (grid cap, wave schedule, store policy, kernel variants).
+// The product library is built without DN_TUNING: every knob reads as unset
+// and the library consults no environment variable.  `make tuning` builds
+// lib/libdn_shamir_tuning.so with -DDN_TUNING, where a knob is the DN_* env
+// var of that name, read per call (scripts/ probes and variant tests only).
+inline const char* tune_env(const char* name) {
+#ifdef DN_TUNING
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 // Record a thread-local error message and return `code` (printf-style).
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 

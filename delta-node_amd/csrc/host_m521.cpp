@@ -230,7 +230,7 @@ uint64_t inv_small(uint64_t a, uint64_t m) {
 
 // DN_EXACT_DIV=0 forces the full-width inverse (A/B and test hook).
 bool exact_div_disabled() {
-  const char* s = std::getenv("DN_EXACT_DIV");
+  const char* s = tune_env("DN_EXACT_DIV");
   return s && s[0] == '0';
 }
 

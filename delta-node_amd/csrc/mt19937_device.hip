@@ -220,7 +220,7 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: %s", hipGetErrorString(err));
   // DN_MT_FORCE_RETRY=1 (test hook) takes the rejected-draw exit so the
   // caller's host fallback can be exercised.
-  const char* fr = std::getenv("DN_MT_FORCE_RETRY");
+  const char* fr = tune_env("DN_MT_FORCE_RETRY");
   if (hflag || (fr && fr[0] == '1'))
     return set_error(DN_ERR_RETRY, "dn_mt19937_draw_coeffs_device: a draw was rejected; redo on the host");
   std::memcpy(mt_state, fin.data(), kMtN * 4);

@@ -158,6 +158,50 @@ __device__ __forceinline__ void prng_coeffs_of(const SplitArgs& a, uint32_t tile
   }
 }
 
+// In place, c becomes the forward-difference table of f at x = 1:
+// synthetic division by (x - z) for z = 1..T-1 turns the monomial
+// coefficients into Newton coefficients b_k on nodes 1, 2, ...
+// (f = b0 + b1 (x-1) + b2 (x-1)(x-2) + ...), and Delta^k f(1) = k! b_k.
+// Every step is c[j] += z * c[j+1] with a small constant z.
+template <int T>
+__device__ __forceinline__ void fd_init(uint32_t c[T][kLimbs]) {
+  if constexpr (T == 3) {
+    // hand-ordered for the headline t = 3 (58 VGPRs, 8 waves/SIMD):
+    // D2 = 2 c2; c2 <- c1 + c2; c1 <- c2 + D2 (= c1 + 3 c2); c2 <- c2 + c0.
+    // (c0 is added last: an int64 secret is 2 live limbs until then.)
+    uint32_t d2[kLimbs];
+    twice(d2, c[2]);
+    add_fe(c[2], c[1]);
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) c[1][i] = c[2][i];
+    add_fe(c[1], d2);
+    add_fe(c[2], c[0]);
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) {
+      c[0][i] = c[2][i];
+      c[2][i] = d2[i];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k + 1 < T; ++k) {
+#pragma unroll
+      for (int j = T - 2; j >= k; --j) {
+        if (k == 0) add_fe(c[j], c[j + 1]);
+        else mul_small_add(c[j], c[j + 1], static_cast<uint32_t>(k + 1), c[j]);
+      }
+    }
+    if constexpr (T >= 3) {
+#pragma unroll
+      for (int k = 2; k < T; ++k) {
+        uint32_t zero[kLimbs];
+#pragma unroll
+        for (int i = 0; i < kLimbs; ++i) zero[i] = 0u;
+        mul_small_add(c[k], c[k], static_cast<uint32_t>(fd_factorial(k)), zero);
+      }
+    }
+  }
+}
+
 constexpr int kMaxPrngT = 8;
 
 template <int T, bool FE_SECRET, bool FOLD, bool PRNG = false, int SAUX = kNt>
@@ -185,46 +229,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
       }
       load_secret<FE_SECRET>(a, tile, w, c[0]);
       if constexpr (!FOLD) {
-        // In place, c becomes the forward-difference table at x = 1:
-        // synthetic division by (x - z) for z = 1..T-1 turns the monomial
-        // coefficients into Newton coefficients b_k on nodes 1, 2, ...
-        // (f = b0 + b1 (x-1) + b2 (x-1)(x-2) + ...), and Delta^k f(1) = k! b_k.
-        // Every step is c[j] += z * c[j+1] with a small constant z.
-        if constexpr (T == 3) {
-          // hand-ordered for the headline t = 3 (58 VGPRs, 8 waves/SIMD):
-          // D2 = 2 c2; c2 <- c1 + c2; c1 <- c2 + D2 (= c1 + 3 c2); c2 <- c2 + c0.
-          // (c0 is added last: an int64 secret is 2 live limbs until then.)
-          uint32_t d2[kLimbs];
-          twice(d2, c[2]);
-          add_fe(c[2], c[1]);
-#pragma unroll
-          for (int i = 0; i < kLimbs; ++i) c[1][i] = c[2][i];
-          add_fe(c[1], d2);
-          add_fe(c[2], c[0]);
-#pragma unroll
-          for (int i = 0; i < kLimbs; ++i) {
-            c[0][i] = c[2][i];
-            c[2][i] = d2[i];
-          }
-        } else {
-#pragma unroll
-          for (int k = 0; k + 1 < T; ++k) {
-#pragma unroll
-            for (int j = T - 2; j >= k; --j) {
-              if (k == 0) add_fe(c[j], c[j + 1]);
-              else mul_small_add(c[j], c[j + 1], static_cast<uint32_t>(k + 1), c[j]);
-            }
-          }
-          if constexpr (T >= 3) {
-#pragma unroll
-            for (int k = 2; k < T; ++k) {
-              uint32_t zero[kLimbs];
-#pragma unroll
-              for (int i = 0; i < kLimbs; ++i) zero[i] = 0u;
-              mul_small_add(c[k], c[k], static_cast<uint32_t>(fd_factorial(k)), zero);
-            }
-          }
-        }
+        fd_init<T>(c);
         uint32_t (&D)[T][kLimbs] = c;
 #pragma unroll 1
         for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
@@ -252,6 +257,155 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
           reduce(v);
           store_fe_b(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), w, v);
         }
+      }
+    }
+  }
+}
+
+// ---- wide-access difference-table split ------------------------------------
+// E consecutive elements per lane (E = 2 or 4): lane l of a wave holds tile
+// elements w0 .. w0 + E - 1 with w0 = 64 E g + E l for group g of the tile, so
+// every limb-plane access is one E*4-byte vector per lane and one contiguous
+// 256 E-byte run per wave-instruction (E = 4: a whole 1-KB plane row of the
+// tile, b128; the u16 top plane b64).  A share of a tile is 17 store
+// instructions instead of 68.  The arithmetic is split_kernel<T, false,
+// false>'s, per element.  A partial last tile takes the one-element path.
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int E>
+__device__ __forceinline__ void load_planes_wide(rsrc_t r, uint32_t o4, uint32_t c[E][kLimbs]) {
+  static_assert(E == 2 || E == 4, "E");
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if constexpr (E == 4) {
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, o4, i * 4 * kTile, kNt);
+      c[0][i] = v.x, c[1][i] = v.y, c[2][i] = v.z, c[3][i] = v.w;
+    } else {
+      const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, o4, i * 4 * kTile, kNt);
+      c[0][i] = v.x, c[1][i] = v.y;
+    }
+  }
+  const int ho = static_cast<int>(kHiOffset);
+  if constexpr (E == 4) {
+    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(r, o4 >> 1, ho, kNt);
+    c[0][16] = v.x & kTopMask, c[1][16] = (v.x >> 16) & kTopMask;
+    c[2][16] = v.y & kTopMask, c[3][16] = (v.y >> 16) & kTopMask;
+  } else {
+    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(r, o4 >> 1, ho, kNt);
+    c[0][16] = v & kTopMask, c[1][16] = (v >> 16) & kTopMask;
+  }
+}
+
+// Store f = D (lazy, < 2^544) of E elements as canonical residues (as
+// store_reduced, for E elements at once: if any lane of the wave needs more
+// than the one-limb fold, the whole wave reduces its D in place).
+template <int T, int E>
+__device__ __forceinline__ void store_reduced_wide(rsrc_t r, uint32_t o4, uint32_t D[E][T][kLimbs]) {
+  uint32_t l0[E], top[E];
+  bool rare = false;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    unsigned c;
+    top[e] = D[e][0][16] & kTopMask;
+    l0[e] = __builtin_addc(D[e][0][0], D[e][0][16] >> 9, 0u, &c);
+    rare |= (c != 0u) || (top[e] == kTopMask);
+  }
+  if (__builtin_expect(__ballot(rare) != 0ull, 0)) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      reduce(D[e][0]);
+      l0[e] = D[e][0][0];
+      top[e] = D[e][0][16];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if constexpr (E == 4) {
+      u32x4_t v;
+      v.x = i ? D[0][0][i] : l0[0], v.y = i ? D[1][0][i] : l0[1];
+      v.z = i ? D[2][0][i] : l0[2], v.w = i ? D[3][0][i] : l0[3];
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, o4, i * 4 * kTile, kNt);
+    } else {
+      u32x2_t v;
+      v.x = i ? D[0][0][i] : l0[0], v.y = i ? D[1][0][i] : l0[1];
+      __builtin_amdgcn_raw_buffer_store_b64(v, r, o4, i * 4 * kTile, kNt);
+    }
+  }
+  const int ho = static_cast<int>(kHiOffset);
+  if constexpr (E == 4) {
+    u32x2_t v;
+    v.x = top[0] | (top[1] << 16), v.y = top[2] | (top[3] << 16);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, o4 >> 1, ho, kNt);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(top[0] | (top[1] << 16), r, o4 >> 1, ho, kNt);
+  }
+}
+
+template <int T, int E>
+__global__ void __launch_bounds__(kBlock) split_wide_kernel(const SplitArgs a) {
+  static_assert(T >= 2 && (E == 2 || E == 4), "wide split: t >= 2, E = 2 or 4");
+  constexpr uint32_t kGroups = kTile / (64 * E);
+  const uint32_t lane = threadIdx.x & 63u;
+  const WaveSched ws = wave_sched(a.tile_map == 3u ? 0u : a.tile_map, a.ntiles);
+  for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
+    if (static_cast<uint64_t>(tile + 1) * kTile > a.n_elem) {
+      // partial last tile: one element per lane (split_kernel's path)
+#pragma unroll 1
+      for (uint32_t q = 0; q < 4u; ++q) {
+        const uint32_t w = lane + 64u * q;
+        if (static_cast<uint64_t>(tile) * kTile + w >= a.n_elem) break;
+        uint32_t c[T][kLimbs];
+#pragma unroll
+        for (int j = 1; j < T; ++j)
+          load_fe_b(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.coeff_stride, tile)), w, c[j]);
+        load_secret<false>(a, tile, w, c[0]);
+        fd_init<T>(c);
+#pragma unroll 1
+        for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+          store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), w, c[0]);
+          fd_step<T>(c);
+        }
+      }
+      continue;
+    }
+#pragma unroll 1
+    for (uint32_t g = 0; g < kGroups; ++g) {
+      const uint32_t w0 = 64u * E * g + E * lane;
+      const uint32_t o4 = 4u * w0;
+      uint32_t c[E][T][kLimbs];
+#pragma unroll
+      for (int j = 1; j < T; ++j) {
+        uint32_t cj[E][kLimbs];
+        load_planes_wide<E>(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.coeff_stride, tile)), o4,
+                            cj);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int i = 0; i < kLimbs; ++i) c[e][j][i] = cj[e][i];
+      }
+      {
+        const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int64_t*>(a.sec_u64 + static_cast<uint64_t>(tile) * kTile), 0, kTile * 8, 0x00020000);
+#pragma unroll
+        for (int h = 0; h < E / 2; ++h) {
+          const u32x4_t s = __builtin_amdgcn_raw_buffer_load_b128(rs, 8u * w0 + 16u * h, 0, kNt);
+          c[2 * h][0][0] = s.x, c[2 * h][0][1] = s.y;
+          c[2 * h + 1][0][0] = s.z, c[2 * h + 1][0][1] = s.w;
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int i = 2; i < kLimbs; ++i) c[e][0][i] = 0u;
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) fd_init<T>(c[e]);
+#pragma unroll 1
+      for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+        store_reduced_wide<T, E>(
+            tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), o4, c);
+#pragma unroll
+        for (int e = 0; e < E; ++e) fd_step<T>(c[e]);
       }
     }
   }
@@ -416,7 +570,7 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
 
 // DN_RECON_UNROLL=0 selects the runtime-k kernel (A/B hook, read per call).
 static bool recon_unroll() {
-  const char* e = std::getenv("DN_RECON_UNROLL");
+  const char* e = tune_env("DN_RECON_UNROLL");
   return !(e && e[0] == '0');
 }
 
@@ -456,7 +610,7 @@ static int cu_count() {
 // L2 / EA path; DESIGN.md §5.1, profiles/r01/placement/).
 // DN_GRID_CAP overrides both (read per call; used by the tuning scripts).
 static int grid_for(uint64_t ntiles, bool per_cu = false) {
-  const char* s = std::getenv("DN_GRID_CAP");
+  const char* s = tune_env("DN_GRID_CAP");
   const int v = s ? std::atoi(s) : 0;
   const uint64_t cap = v > 0 ? static_cast<uint64_t>(v) : per_cu ? static_cast<uint64_t>(cu_count()) : 16384u;
   const uint64_t blocks = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -467,7 +621,7 @@ static int grid_for(uint64_t ntiles, bool per_cu = false) {
 // default 0.  Mode 1 needs grid % 8 == 0; the PRNG kernels (one wave per tile
 // for the shared top-limb blocks) cannot use mode 3.
 static uint32_t tile_map_for(int grid, bool allow_coop = true) {
-  const char* s = std::getenv("DN_TILE_MAP");
+  const char* s = tune_env("DN_TILE_MAP");
   const uint32_t m = (s && s[0] >= '0' && s[0] <= '3') ? static_cast<uint32_t>(s[0] - '0') : 0u;
   if (m == 1u && grid % static_cast<int>(kXcds) != 0) return 0u;
   if (m == 3u && !allow_coop) return 0u;
@@ -498,8 +652,9 @@ static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
     case 1: hipLaunchKernelGGL((split_kernel<1, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
     case 2: hipLaunchKernelGGL((split_kernel<2, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
     case 3: {
-      // DN_STORE_AUX (A/B hook): cache policy bits of the share stores, headline kernel only
-      const char* sa = (!FE_SECRET && !FOLD) ? std::getenv("DN_STORE_AUX") : nullptr;
+#ifdef DN_TUNING
+      // DN_STORE_AUX (tuning build): cache policy bits of the share stores, headline kernel only
+      const char* sa = (!FE_SECRET && !FOLD) ? tune_env("DN_STORE_AUX") : nullptr;
       const int aux = sa ? std::atoi(sa) : kNt;
       if (aux == 0) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 0>), g, dim3(kBlock), 0, s, a);
       else if (aux == 1) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 1>), g, dim3(kBlock), 0, s, a);
@@ -508,7 +663,9 @@ static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
       else if (aux == 17) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 17>), g, dim3(kBlock), 0, s, a);
       else if (aux == 18) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 18>), g, dim3(kBlock), 0, s, a);
       else if (aux == 19) hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD, false, 19>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a);
+      else
+#endif
+      hipLaunchKernelGGL((split_kernel<3, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a);
       break;
     }
     case 4: hipLaunchKernelGGL((split_kernel<4, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
@@ -518,6 +675,29 @@ static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
     case 8: hipLaunchKernelGGL((split_kernel<8, FE_SECRET, FOLD>), g, dim3(kBlock), 0, s, a); break;
     default: hipLaunchKernelGGL((split_kernel_generic<FE_SECRET>), g, dim3(kBlock), 0, s, a); break;
   }
+}
+
+// Elements per lane of the difference-table split with int64 secrets
+// (0: the one-element split_kernel).  DN_SPLIT_E (tuning build) overrides.
+// Measured (scripts/split_wide_probe.py, profiles/r02/split_wide.jsonl; the
+// same three share allocations each): t = 3, n = 5 — one element per lane is
+// fastest (1.48-1.49 ms at 2^24 vs 1.51-1.57 for E = 2 / 4, every grid cap),
+// already at 98-101 % of the same-buffer 16-B streaming ceiling; t = 5, n = 9
+// — E = 2 is 4.7 % faster where the share buffer's placement is fast (2.42 vs
+// 2.54 ms) and within 1 % where it is slow.
+static int split_wide_e(int t) {
+  const char* e = tune_env("DN_SPLIT_E");
+  if (e) return std::atoi(e);
+  return t == 5 ? 2 : 0;
+}
+
+static bool launch_split_wide(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
+  const int E = split_wide_e(t);
+  if (E == 4 && t == 3) hipLaunchKernelGGL((split_wide_kernel<3, 4>), g, dim3(kBlock), 0, s, a);
+  else if (E == 2 && t == 3) hipLaunchKernelGGL((split_wide_kernel<3, 2>), g, dim3(kBlock), 0, s, a);
+  else if (E == 2 && t == 5) hipLaunchKernelGGL((split_wide_kernel<5, 2>), g, dim3(kBlock), 0, s, a);
+  else return false;
+  return true;
 }
 
 template <bool FOLD>
@@ -575,16 +755,13 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
     return set_error(DN_ERR_ARG, "%s: null pointer", name);
   a.ntiles = (a.n_elem + kTile - 1) / kTile;
   a.vec_bytes = a.ntiles * kTileBytes;
-  {  // DN_ROW_PAD: experimental row pitch = vec_bytes + pad (placement probe only)
-    const char* rp = std::getenv("DN_ROW_PAD");
-    const uint64_t pad = rp ? std::strtoull(rp, nullptr, 10) : 0;
-    a.coeff_stride = a.vec_bytes + pad;
-    a.share_stride = a.vec_bytes + pad;
-  }
+  // rows of the caller's [t-1, vec_bytes] / [n, vec_bytes] blocks are dense
+  a.coeff_stride = a.vec_bytes;
+  a.share_stride = a.vec_bytes;
   a.n_shares = n_shares;
   a.threshold = threshold;
   // DN_SPLIT_HORNER=1 forces the Horner kernel (A/B hook, read per call).
-  const char* hz = std::getenv("DN_SPLIT_HORNER");
+  const char* hz = tune_env("DN_SPLIT_HORNER");
   const bool fold_each = needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
   const bool per_cu = !prng && !fold_each && threshold <= 8;  // the memory-bound difference-table kernels
   const dim3 g(grid_for(a.ntiles, per_cu));
@@ -596,6 +773,7 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   } else if (fe) {
     if (fold_each) launch_split_t<true, true>(threshold, g, s, a);
     else launch_split_t<true, false>(threshold, g, s, a);
+  } else if (!fold_each && launch_split_wide(threshold, g, s, a)) {
   } else {
     if (fold_each) launch_split_t<false, true>(threshold, g, s, a);
     else launch_split_t<false, false>(threshold, g, s, a);

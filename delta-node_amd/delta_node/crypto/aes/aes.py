@@ -37,13 +37,9 @@ from ..shamir import _native
 
 EXPORTS = ("dn_aes_expand_key", "dn_aes_ctr", "dn_aes_encrypt_len", "dn_aes_encrypt", "dn_aes_decrypt_capacity",
            "dn_aes_decrypt")
-_bound = False
-
-
 def _lib() -> ctypes.CDLL:
-    global _bound
     L = _native.lib()
-    if not _bound:
+    if not getattr(L, "_dn_aes_bound", False):  # argtypes, once per loaded library
         vp, u64, i32, cp = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p
         L.dn_aes_expand_key.restype = i32
         L.dn_aes_expand_key.argtypes = [cp, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32)]
@@ -57,7 +53,7 @@ def _lib() -> ctypes.CDLL:
         L.dn_aes_decrypt_capacity.argtypes = [u64, i32]
         L.dn_aes_decrypt.restype = i32
         L.dn_aes_decrypt.argtypes = [cp, i32, vp, u64, i32, vp, u64, vp, vp, vp]
-        _bound = True
+        L._dn_aes_bound = True
     return L
 
 

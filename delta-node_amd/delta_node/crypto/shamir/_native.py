@@ -10,6 +10,7 @@ loaded (same soname), i.e. one runtime, one set of streams per process.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -77,47 +78,69 @@ def lib() -> ctypes.CDLL:
     if _lib is not None:
         return _lib
     with _lock:
-        if _lib is not None:
-            return _lib
-        import torch  # noqa: F401  (bind the HIP runtime torch already loaded)
+        if _lib is None:
+            _lib = _load(lib_path())
+        return _lib
 
-        path = lib_path()
-        if not os.path.exists(path):
-            raise RuntimeError(
-                f"libdn_shamir.so not found at {path}: build it with `make -C delta-node_amd` "
-                "(or __graft_entry__.build()); the Shamir hot path has no CPU fallback")
-        L = ctypes.CDLL(path)
-        vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
-        L.dn_m521_vec_bytes.restype = u64
-        L.dn_m521_vec_bytes.argtypes = [u64]
-        L.dn_m521_split_u64.restype = i32
-        L.dn_m521_split_u64.argtypes = [vp, vp, vp, u64, i32, i32, vp]
-        L.dn_m521_split_fe.restype = i32
-        L.dn_m521_split_fe.argtypes = [vp, vp, vp, u64, i32, i32, vp]
-        L.dn_m521_lagrange.restype = i32
-        L.dn_m521_split_prng.restype = i32
-        L.dn_m521_split_prng.argtypes = [vp, vp, u64, i32, u64, vp, u64, i32, i32, vp]
-        L.dn_m521_prng_coeffs.restype = i32
-        L.dn_m521_prng_coeffs.argtypes = [vp, u64, i32, u64, vp, u64, i32, vp]
-        L.dn_m521_lagrange.argtypes = [ctypes.POINTER(ctypes.c_uint64), i32, i32, ctypes.POINTER(Lagrange)]
-        L.dn_m521_reconstruct.restype = i32
-        L.dn_m521_reconstruct.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(Lagrange), vp, vp, vp, u64, vp]
-        L.dn_mt19937_draw_coeffs.restype = i32
-        L.dn_mt19937_draw_coeffs.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64,
-                                             i32, vp]
-        L.dn_mt19937_device_scratch_bytes.restype = u64
-        L.dn_mt19937_device_scratch_bytes.argtypes = [u64, i32]
-        L.dn_mt19937_draw_coeffs_device.restype = i32
-        L.dn_mt19937_draw_coeffs_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
-                                                    u64, i32, vp, vp, u64, vp]
-        L.dn_mt19937_skip.restype = i32
-        L.dn_mt19937_skip.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64]
-        L.dn_last_error.restype = ctypes.c_char_p
-        L.dn_last_error.argtypes = []
-        L.dn_version.restype = ctypes.c_char_p
-        L.dn_version.argtypes = []
-        _lib = L
-        return L
+
+@contextlib.contextmanager
+def library(path: str):
+    """Bind another build of the same C-ABI for the duration of a block —
+    the tuning build (lib/libdn_shamir_tuning.so, whose DN_* knobs select
+    kernel variants) in the variant-equivalence tests.  Not thread-safe; the
+    product library is restored on exit."""
+    global _lib
+    prev = lib()
+    with _lock:
+        _lib = _load(path)
+    try:
+        yield _lib
+    finally:
+        with _lock:
+            _lib = prev
+
+
+TUNING_LIB = os.path.join(os.path.dirname(DEFAULT_LIB), "libdn_shamir_tuning.so")
+
+
+def _load(path: str) -> ctypes.CDLL:
+    import torch  # noqa: F401  (bind the HIP runtime torch already loaded)
+
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libdn_shamir.so not found at {path}: build it with `make -C delta-node_amd` "
+            "(or __graft_entry__.build()); the Shamir hot path has no CPU fallback")
+    L = ctypes.CDLL(path)
+    vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    L.dn_m521_vec_bytes.restype = u64
+    L.dn_m521_vec_bytes.argtypes = [u64]
+    L.dn_m521_split_u64.restype = i32
+    L.dn_m521_split_u64.argtypes = [vp, vp, vp, u64, i32, i32, vp]
+    L.dn_m521_split_fe.restype = i32
+    L.dn_m521_split_fe.argtypes = [vp, vp, vp, u64, i32, i32, vp]
+    L.dn_m521_lagrange.restype = i32
+    L.dn_m521_split_prng.restype = i32
+    L.dn_m521_split_prng.argtypes = [vp, vp, u64, i32, u64, vp, u64, i32, i32, vp]
+    L.dn_m521_prng_coeffs.restype = i32
+    L.dn_m521_prng_coeffs.argtypes = [vp, u64, i32, u64, vp, u64, i32, vp]
+    L.dn_m521_lagrange.argtypes = [ctypes.POINTER(ctypes.c_uint64), i32, i32, ctypes.POINTER(Lagrange)]
+    L.dn_m521_reconstruct.restype = i32
+    L.dn_m521_reconstruct.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(Lagrange), vp, vp, vp, u64, vp]
+    L.dn_mt19937_draw_coeffs.restype = i32
+    L.dn_mt19937_draw_coeffs.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64,
+                                         i32, vp]
+    L.dn_mt19937_device_scratch_bytes.restype = u64
+    L.dn_mt19937_device_scratch_bytes.argtypes = [u64, i32]
+    L.dn_mt19937_draw_coeffs_device.restype = i32
+    L.dn_mt19937_draw_coeffs_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
+                                                u64, i32, vp, vp, u64, vp]
+    L.dn_mt19937_skip.restype = i32
+    L.dn_mt19937_skip.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64]
+    L.dn_last_error.restype = ctypes.c_char_p
+    L.dn_last_error.argtypes = []
+    L.dn_version.restype = ctypes.c_char_p
+    L.dn_version.argtypes = []
+    return L
 
 
 def last_error() -> str:

@@ -18,13 +18,9 @@ from . import _native, field
 
 EXPORTS = ("dn_m521_codec_scratch_bytes", "dn_m521_encoded_capacity", "dn_m521_encode_shares",
            "dn_m521_decode_shares")
-_bound = False
-
-
 def _lib():
-    global _bound
     L = _native.lib()
-    if not _bound:
+    if not getattr(L, "_dn_codec_bound", False):  # argtypes, once per loaded library
         vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
         L.dn_m521_codec_scratch_bytes.restype = u64
         L.dn_m521_codec_scratch_bytes.argtypes = [u64]
@@ -34,7 +30,7 @@ def _lib():
         L.dn_m521_encode_shares.argtypes = [vp, u64, u64, vp, vp, u64, vp, u64, vp]
         L.dn_m521_decode_shares.restype = i32
         L.dn_m521_decode_shares.argtypes = [vp, u64, vp, u64, vp, vp, vp, vp]
-        _bound = True
+        L._dn_codec_bound = True
     return L
 
 

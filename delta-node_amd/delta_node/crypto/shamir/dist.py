@@ -35,6 +35,15 @@ def shard_tiles(n_total: int, world: int) -> int:
     return (tiles + world - 1) // world
 
 
+def _via_host(t, group) -> bool:
+    """gloo is a host transport: device tensors are gathered through host
+    memory (the multi-rank GPU tests run every rank on one GPU with gloo; the
+    product backend is nccl = RCCL, which moves device memory directly)."""
+    import torch.distributed as dist
+
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def allgather_share_blocks(local_block, n_total: int, group=None):
     """Gather every rank's share block into full share vectors on every rank.
 
@@ -56,11 +65,12 @@ def allgather_share_blocks(local_block, n_total: int, group=None):
     S, B = local_block.shape
     if B != shard_tiles(n_total, world) * field.TILE_BYTES:
         raise ValueError("allgather_share_blocks: block is not padded to the common shard size")
-    src = local_block.contiguous()
-    out = torch.empty((S, world * B), dtype=local_block.dtype, device=local_block.device)
+    host = _via_host(local_block, group)
+    src = local_block.cpu() if host else local_block.contiguous()
+    out = torch.empty((S, world * B), dtype=local_block.dtype, device=src.device)
     for s in range(S):
         dist.all_gather_into_tensor(out[s], src[s], group=group)
-    return out
+    return out.to(local_block.device) if host else out
 
 
 def draw_coeffs_sharded(ss, n_total: int, device=None, group=None):
@@ -96,6 +106,8 @@ def draw_coeffs_sharded(ss, n_total: int, device=None, group=None):
         _native.mt_skip(ss.random, 17 * tm1 * n_total)
         rejected = False
     flag = torch.tensor([int(rejected)], dtype=torch.int32, device=out.device)
+    if _via_host(flag, group):
+        flag = flag.cpu()
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     if int(flag.item()):
         from . import _native

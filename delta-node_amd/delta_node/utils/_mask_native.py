@@ -26,13 +26,9 @@ class PCG64(ctypes.Structure):
         return (self.inc_hi << 64) | self.inc_lo
 
 
-_bound = False
-
-
 def lib() -> ctypes.CDLL:
-    global _bound
     L = _native.lib()
-    if not _bound:
+    if not getattr(L, "_dn_mask_bound", False):  # argtypes, once per loaded library
         vp, u64, i32, i64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int64
         L.dn_pcg64_seed.restype = i32
         L.dn_pcg64_seed.argtypes = [ctypes.POINTER(ctypes.c_uint32), i32, ctypes.POINTER(PCG64)]
@@ -48,7 +44,7 @@ def lib() -> ctypes.CDLL:
         L.dn_i64_sum.argtypes = [ctypes.POINTER(vp), i32, vp, u64, vp]
         L.dn_unfix_precision.restype = i32
         L.dn_unfix_precision.argtypes = [vp, vp, u64, i32, vp]
-        _bound = True
+        L._dn_mask_bound = True
     return L
 
 

@@ -22,13 +22,9 @@ __all__ = ["calc_weight_commitment", "calc_data_commitment"]
 Q = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 DATA_BLOCK = 128
 EXPORTS = ("dn_mimc7_data_rows", "dn_mimc7_merkle_blocks", "dn_mimc7_weight_chain", "dn_mimc7_hash")
-_bound = False
-
-
 def _lib():
-    global _bound
     L = _native.lib()
-    if not _bound:
+    if not getattr(L, "_dn_mimc7_bound", False):  # argtypes, once per loaded library
         vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
         L.dn_mimc7_data_rows.restype = i32
         L.dn_mimc7_data_rows.argtypes = [vp, u64, i32, vp, vp, vp]
@@ -38,7 +34,7 @@ def _lib():
         L.dn_mimc7_weight_chain.argtypes = [vp, u64, i32, vp, vp, vp]
         L.dn_mimc7_hash.restype = i32
         L.dn_mimc7_hash.argtypes = [vp, vp, u64, vp, vp]
-        _bound = True
+        L._dn_mimc7_bound = True
     return L
 
 

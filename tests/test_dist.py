@@ -1,10 +1,12 @@
 """Multi-process element sharding (CPU, gloo, world_size 2 and 3).
 
-Each rank computes the shares of its tile-aligned shard (here with the C
-oracle standing in for the per-rank kernel — the device kernels are covered by
-the gpu tests), packs them into its padded block and all-gathers; the
-gathered vectors must equal the unsharded split byte for byte.  This is the
-data path `bench.py --allgather` and BASELINE config 4 use over RCCL.
+Each rank computes the shares of its tile-aligned shard (here, on a CPU-only
+host, with the C oracle standing in for the per-rank kernel), packs them into
+its padded block and all-gathers; the gathered vectors must equal the
+unsharded split byte for byte.  This is the data path `bench.py` and BASELINE
+config 4 use over RCCL.  The same path with the HIP kernels — device MT
+draw per shard, HIP split, gather, reconstruct — runs in tests/test_gpu_dist.py
+(fresh child ranks on one GPU, gloo).
 """
 import os
 import socket

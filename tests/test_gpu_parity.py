@@ -245,9 +245,10 @@ def test_reconstruct_exact_division_equals_full_inverse(xs, monkeypatch):
     outs = {}
     for mode in ("1", "0"):
         monkeypatch.setenv("DN_EXACT_DIV", mode)
-        w = _native.lagrange(xs, k)
-        res = torch.empty(field.vec_bytes(N), dtype=torch.uint8, device=dev())
-        _native.reconstruct(vecs, w, out_fe=res, n=N)
+        with _native.library(_native.TUNING_LIB):  # DN_EXACT_DIV is a tuning-build knob
+            w = _native.lagrange(xs, k)
+            res = torch.empty(field.vec_bytes(N), dtype=torch.uint8, device=dev())
+            _native.reconstruct(vecs, w, out_fe=res, n=N)
         outs[(mode, w.has_inv)] = field.vec_to_limbs(res.cpu().numpy(), N)
     assert {m for m, _ in outs} == {"1", "0"}
     vals = list(outs.values())
@@ -334,7 +335,9 @@ def test_tile_map_and_grid_cap_do_not_change_results(N, cap, monkeypatch):
     multiple of 8 fall back —, blocked runs, workgroup-cooperative quarters) and
     small grid caps (several grid-stride passes) give the same shares and
     reconstructions, equal to the C oracle; the device-PRNG split too (mode 3
-    falls back to 0 there)."""
+    falls back to 0 there); so do the wide-access splits (DN_SPLIT_E = 2, 4
+    consecutive elements per lane), partial last tiles included.  These are
+    knobs of the tuning build (lib/libdn_shamir_tuning.so)."""
     t, n = 3, 5
     sec = secrets_int64(N + cap, N)
     ss = shamir.SecretShare(t)
@@ -343,19 +346,25 @@ def test_tile_map_and_grid_cap_do_not_change_results(N, cap, monkeypatch):
     secd = torch.from_numpy(sec).to(dev())
     if cap:
         monkeypatch.setenv("DN_GRID_CAP", str(cap))
-    outs, prng = [], []
-    key = bytes(range(32))
-    for m in ("0", "1", "2", "3"):
-        monkeypatch.setenv("DN_TILE_MAP", m)
-        ps = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
-        _native.split_prng(secd, key, 7, 20, 0, ps, N, t, n)
-        prng.append(block_limbs(ps, N))
-        shares = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
-        _native.split_u64(secd, coeffs, shares, N, t, n)
-        rec = torch.empty(N, dtype=torch.int64, device=dev())
-        _native.reconstruct([shares[1], shares[2], shares[4]], _native.lagrange([2, 3, 5], t), out_u64=rec, n=N)
-        assert torch.equal(rec, secd)
-        outs.append(shares)
+    with _native.library(_native.TUNING_LIB):
+        outs, prng = [], []
+        key = bytes(range(32))
+        variants = [("0", None), ("1", None), ("2", None), ("3", None), ("0", "2"), ("0", "4"), ("2", "4")]
+        for m, wide in variants:
+            monkeypatch.setenv("DN_TILE_MAP", m)
+            if wide:
+                monkeypatch.setenv("DN_SPLIT_E", wide)
+            else:
+                monkeypatch.delenv("DN_SPLIT_E", raising=False)
+            ps = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
+            _native.split_prng(secd, key, 7, 20, 0, ps, N, t, n)
+            prng.append(block_limbs(ps, N))
+            shares = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
+            _native.split_u64(secd, coeffs, shares, N, t, n)
+            rec = torch.empty(N, dtype=torch.int64, device=dev())
+            _native.reconstruct([shares[1], shares[2], shares[4]], _native.lagrange([2, 3, 5], t), out_u64=rec, n=N)
+            assert torch.equal(rec, secd)
+            outs.append(shares)
     for o in outs[1:]:
         assert np.array_equal(block_limbs(outs[0], N), block_limbs(o, N))  # valid elements
     for o in prng[1:]:
@@ -398,20 +407,21 @@ def test_draw_coeffs_vec_device_path_matches_reference_fixture():
 
 
 def test_device_mt_draw_falls_back_to_host_on_retry(monkeypatch):
-    """The rejected-draw exit (DN_ERR_RETRY, forced by the test hook) leaves the
-    state untouched and draw_coeffs_vec redoes the draw on the host: same block,
-    same final state as the host draw."""
+    """The rejected-draw exit (DN_ERR_RETRY, forced by the tuning build's
+    DN_MT_FORCE_RETRY) leaves the state untouched and draw_coeffs_vec redoes
+    the draw on the host: same block, same final state as the host draw."""
     n = 50000
     a, b = random.Random(77), random.Random(77)
     want = _native.mt_draw_coeffs(a, n, 2)
     monkeypatch.setenv("DN_MT_FORCE_RETRY", "1")
-    blk = torch.zeros((2, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
-    state0 = b.getstate()
-    assert not _native.mt_draw_coeffs_device(b, n, 2, blk)
-    assert b.getstate() == state0
-    ss = shamir.SecretShare(3)
-    ss.random.setstate(state0)
-    got = ss.draw_coeffs_vec(n, dev())
+    with _native.library(_native.TUNING_LIB):
+        blk = torch.zeros((2, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+        state0 = b.getstate()
+        assert not _native.mt_draw_coeffs_device(b, n, 2, blk)
+        assert b.getstate() == state0
+        ss = shamir.SecretShare(3)
+        ss.random.setstate(state0)
+        got = ss.draw_coeffs_vec(n, dev())
     assert np.array_equal(got.cpu().numpy(), want)
     assert ss.random.getstate() == a.getstate()
 

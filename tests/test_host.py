@@ -152,11 +152,36 @@ def test_lagrange_fast_forms():
 
 
 def test_lagrange_full_inverse_form(monkeypatch):
+    """The full-width inverse form (tuning build, DN_EXACT_DIV=0) describes the
+    same weights as the reference's."""
     monkeypatch.setenv("DN_EXACT_DIV", "0")
-    for xs in ([2, 4, 5], [1, 2, 4, 5], [7, 100, 255], [2, 3, 5, 8, 9]):
-        w = _native.lagrange(xs, 0)
-        assert w.has_inv in (0, 1)
-        assert _lam_from_desc(w) == _lam_ref(xs)
+    with _native.library(_native.TUNING_LIB):
+        for xs in ([2, 4, 5], [1, 2, 4, 5], [7, 100, 255], [2, 3, 5, 8, 9]):
+            w = _native.lagrange(xs, 0)
+            assert w.has_inv in (0, 1)
+            assert _lam_from_desc(w) == _lam_ref(xs)
+
+
+def test_product_library_reads_no_environment(monkeypatch):
+    """The product library consults no DN_* knob (they exist only in the
+    tuning build): it imports no getenv, and a set knob changes nothing."""
+    import shutil
+    import subprocess
+
+    if shutil.which("nm"):
+        und = subprocess.run(["nm", "-D", "--undefined-only", _native.lib_path()], capture_output=True, text=True,
+                             check=True).stdout
+        assert "getenv" not in und and "secure_getenv" not in und
+        und_t = subprocess.run(["nm", "-D", "--undefined-only", _native.TUNING_LIB], capture_output=True, text=True,
+                               check=True).stdout
+        assert "getenv" in und_t
+    want = _native.lagrange([2, 4, 5], 3)
+    for k, v in (("DN_EXACT_DIV", "0"), ("DN_GRID_CAP", "7"), ("DN_TILE_MAP", "3"), ("DN_SPLIT_E", "4")):
+        monkeypatch.setenv(k, v)
+    got = _native.lagrange([2, 4, 5], 3)
+    assert (got.has_inv, got.d, got.shift) == (want.has_inv, want.d, want.shift) == (2, 3, 0)
+    with _native.library(_native.TUNING_LIB):
+        assert _native.lagrange([2, 4, 5], 3).has_inv in (0, 1)  # the knob works where it exists
 
 
 def test_lagrange_errors_mirror_reference():
