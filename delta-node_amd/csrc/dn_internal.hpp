@@ -28,11 +28,10 @@ int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3
 int device_cu_count();
 
 // MT19937 jump-ahead (host_mt_jump.cpp): substream length in words, the most
-// substreams the jump table covers, substream start windows and CPython's
-// final state after `words` outputs (wins may be null).
+// substreams the jump table covers, a window stepped forward on the host, and
+// CPython's final state after `words` outputs (false: beyond the table).
 uint64_t mt_jump_words();
 uint64_t mt_jump_max_subs();
-void mt_build_windows(const uint32_t* state, int idx, uint64_t subs, uint32_t* wins);
-void mt_final_state(const uint32_t* state, int idx, uint64_t words, const uint32_t* wins, uint64_t subs,
-                    uint32_t* fin, int32_t* fidx);
+void mt_advance_window(const uint32_t* win, uint64_t steps, uint32_t* out);
+bool mt_final_state(const uint32_t* state, int idx, uint64_t words, uint32_t* fin, int32_t* fidx);
 }  // namespace dn

@@ -8,7 +8,6 @@
 // (Haramoto et al., INFORMS J. Computing 20(3), 2008).
 #include <cstdint>
 #include <cstring>
-#include <thread>
 #include <vector>
 
 #include "dn_internal.hpp"
@@ -17,6 +16,8 @@ namespace dn {
 namespace {
 
 #include "mt19937_jump.inc"
+
+alignas(64) static const uint64_t kMtJumpPolys[kMtJumpRows][kMtPolyWords] = DN_MT_JUMP_POLYS;
 
 constexpr int kMtN = 624, kMtM = 397;
 constexpr uint32_t kMtA = 0x9908b0dfu, kMtUp = 0x80000000u, kMtLo = 0x7fffffffu;
@@ -88,99 +89,64 @@ void mt_jump(const uint32_t* win, const uint64_t* g, uint32_t* out) {
   std::memcpy(out, buf.data() + p, kMtN * sizeof(uint32_t));
 }
 
-// Window 1 + d (time B + (1 + d) L - h) from window 1 by the binary
-// decomposition of d (jumps of 2^k L; beyond the table, repeated top jumps).
-void mt_window_from1(const uint32_t* w1, uint64_t d, uint32_t* out) {
-  std::vector<uint32_t> cur(w1, w1 + kMtN), nxt(kMtN);
-  for (int lev = 0; d; ++lev, d >>= 1) {
-    if (lev == kMtJumpLevels - 1) {  // the rest: d times 2^lev L
-      for (uint64_t r = 0; r < d; ++r) {
-        mt_jump(cur.data(), kMtJumpPolys[1 + lev], nxt.data());
-        cur.swap(nxt);
-      }
-      break;
-    }
-    if (d & 1u) {
-      mt_jump(cur.data(), kMtJumpPolys[1 + lev], nxt.data());
-      cur.swap(nxt);
-    }
+// The window of substream s >= 1: buffer positions idx + s L - 624 ..
+// idx + s L - 1, counted from the caller's array (position 0) — s L stream
+// words after the caller's next output, minus one array.  With
+// s - 1 = 4096 c + 64 a + b: A_a, then C_c (c > 0), then B_b (b > 0).
+void mt_window_at(const uint32_t* state, int idx, uint64_t s, uint32_t* out) {
+  std::vector<uint32_t> cur(kMtN), nxt(kMtN);
+  mt_advance(state, static_cast<uint64_t>(idx), cur.data());  // W_idx
+  const uint64_t d = s - 1;
+  const int b = static_cast<int>(d % kMtJumpRadix), a = static_cast<int>((d / kMtJumpRadix) % kMtJumpRadix),
+            c = static_cast<int>(d / (kMtJumpRadix * kMtJumpRadix));
+  mt_jump(cur.data(), kMtJumpPolys[kMtRowA + a], nxt.data());
+  cur.swap(nxt);
+  if (c) {
+    mt_jump(cur.data(), kMtJumpPolys[kMtRowC + c], nxt.data());
+    cur.swap(nxt);
+  }
+  if (b) {
+    mt_jump(cur.data(), kMtJumpPolys[kMtRowB + b], nxt.data());
+    cur.swap(nxt);
   }
   std::memcpy(out, cur.data(), kMtN * sizeof(uint32_t));
-}
-
-// window 1 (time B + L - h): B's window stepped idx words, then L - 624 more
-void mt_window1(const uint32_t* state, int idx, uint32_t* out) {
-  std::vector<uint32_t> adv(kMtN);
-  mt_advance(state, static_cast<uint64_t>(idx), adv.data());
-  mt_jump(adv.data(), kMtJumpPolys[0], out);
 }
 
 }  // namespace
 
 uint64_t mt_jump_words() { return kMtJumpL; }
-uint64_t mt_jump_max_subs() { return 1ull << kMtJumpLevels; }
+uint64_t mt_jump_max_subs() { return 1ull + static_cast<uint64_t>(kMtJumpRadix) * kMtJumpRadix * kMtJumpRadix; }
 
-// Stream words are numbered from CPython's current position: words 0 .. h-1
-// (h = 624 - idx) are the rest of the current array, word w >= h is output
-// w - h of the window at time B (the current array).  Substream s >= 1 starts
-// at word s L, i.e. at the window of time B + s L - h.
-void mt_build_windows(const uint32_t* state, int idx, uint64_t subs, uint32_t* wins) {
-  std::memcpy(wins, state, kMtN * sizeof(uint32_t));
-  if (subs < 2) return;
-  mt_window1(state, idx, wins + kMtN);
-  // window 1 + d for d in [2^lev, 2^(lev+1)) = window 1 + d - 2^lev jumped 2^lev L
-  const unsigned hw = std::thread::hardware_concurrency();
-  const unsigned nthr = hw ? (hw < 16 ? hw : 16) : 1;
-  for (int lev = 0; (1ull << lev) < subs - 1; ++lev) {
-    const uint64_t d0 = 1ull << lev, d1 = (2ull << lev) < subs - 1 ? (2ull << lev) : subs - 1;
-    const uint64_t cnt = d1 - d0;
-    auto work = [&](unsigned t) {
-      for (uint64_t i = t; i < cnt; i += nthr) {
-        const uint64_t d = d0 + i;
-        mt_jump(wins + (1 + d - d0) * kMtN, kMtJumpPolys[1 + lev], wins + (1 + d) * kMtN);
-      }
-    };
-    if (cnt < 4 || nthr == 1) {
-      for (unsigned t = 0; t < nthr; ++t) work(t);
-    } else {
-      std::vector<std::thread> th;
-      for (unsigned t = 0; t < nthr; ++t) th.emplace_back(work, t);
-      for (auto& x : th) x.join();
-    }
-  }
-}
-
-// CPython's state after `words` more outputs: the window at time B + 624 q
-// (q = ceil((words - h) / 624) twists) with index words - h - 624 (q - 1),
-// stepped from the last substream window strictly before it (from `wins` when
-// given — their first word's low bits are not exact, so at least one step).
-void mt_final_state(const uint32_t* state, int idx, uint64_t words, const uint32_t* wins, uint64_t subs,
-                    uint32_t* fin, int32_t* fidx) {
+// CPython's state after `words` more outputs: the array at buffer position
+// 624 q (q = ceil((words - h) / 624) twists, h = 624 - idx) with index
+// words - h - 624 (q - 1), stepped from the last substream window strictly
+// before it (the windows' first word is exact only in its top bit, so at
+// least one step).
+bool mt_final_state(const uint32_t* state, int idx, uint64_t words, uint32_t* fin, int32_t* fidx) {
   const uint64_t h = static_cast<uint64_t>(kMtN - idx);
   if (words <= h) {
     std::memcpy(fin, state, kMtN * sizeof(uint32_t));
     *fidx = idx + static_cast<int32_t>(words);
-    return;
+    return true;
   }
-  const uint64_t m_end = words - h, q = (m_end + kMtN - 1) / kMtN, tf = kMtN * q + h;
-  uint64_t sig = (tf - 1) / kMtJumpL;
-  if (wins && sig > subs - 1) sig = subs - 1;
+  const uint64_t m_end = words - h, q = (m_end + kMtN - 1) / kMtN, tf = kMtN * q;  // buffer position
+  // substream s >= 1 starts at position idx + s L - 624 (mt_window_at)
+  const uint64_t sig = (tf + kMtN - 1 - static_cast<uint64_t>(idx)) / kMtJumpL;  // idx + sig L - 624 < tf
+  if (sig >= mt_jump_max_subs()) return false;  // beyond the jump table (> 1.4e11 words)
   std::vector<uint32_t> w(kMtN);
-  uint64_t t_sig = h;
+  uint64_t t_sig = 0;
   if (sig == 0) {
     std::memcpy(w.data(), state, kMtN * sizeof(uint32_t));
-  } else if (wins) {
-    std::memcpy(w.data(), wins + sig * kMtN, kMtN * sizeof(uint32_t));
-    t_sig = sig * kMtJumpL;
   } else {
-    std::vector<uint32_t> w1(kMtN);
-    mt_window1(state, idx, w1.data());
-    mt_window_from1(w1.data(), sig - 1, w.data());
-    t_sig = sig * kMtJumpL;
+    mt_window_at(state, idx, sig, w.data());
+    t_sig = static_cast<uint64_t>(idx) + sig * kMtJumpL - kMtN;
   }
   mt_advance(w.data(), tf - t_sig, fin);
   *fidx = static_cast<int32_t>(m_end - kMtN * (q - 1));
+  return true;
 }
+
+void mt_advance_window(const uint32_t* win, uint64_t steps, uint32_t* out) { mt_advance(win, steps, out); }
 
 }  // namespace dn
 
@@ -192,7 +158,9 @@ extern "C" int dn_mt19937_skip(uint32_t* mt_state, int32_t* mt_index, uint64_t w
   if (idx < 0 || idx > kMtN) return set_error(DN_ERR_ARG, "dn_mt19937_skip: bad MT index");
   std::vector<uint32_t> fin(kMtN);
   int32_t fidx = 0;
-  mt_final_state(mt_state, idx, words, nullptr, 0, fin.data(), &fidx);
+  if (!mt_final_state(mt_state, idx, words, fin.data(), &fidx))
+    return set_error(DN_ERR_UNSUPPORTED, "dn_mt19937_skip: %llu words exceed the jump table",
+                     static_cast<unsigned long long>(words));
   std::memcpy(mt_state, fin.data(), kMtN * sizeof(uint32_t));
   *mt_index = fidx;
   return DN_OK;

@@ -394,6 +394,23 @@ def test_device_mt_draw_equals_host_draw(n, tm1, pre):
     assert a.getstate() == b.getstate()
 
 
+@pytest.mark.slow
+def test_device_mt_draw_equals_host_draw_past_4096_substreams():
+    """2^26 elements x 4 coefficients (BASELINE config 4's draw: 8192
+    substreams, so the windows past 4097 take all three jump levels A, C, B):
+    byte-equal to the sequential host draw, same final random.Random state."""
+    n, tm1 = 1 << 26, 4
+    a = random.Random(4321)
+    a.getrandbits(32 * 100)
+    b = random.Random()
+    b.setstate(a.getstate())
+    got = torch.empty((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    assert _native.mt_draw_coeffs_device(b, n, tm1, got)
+    want = torch.from_numpy(_native.mt_draw_coeffs(a, n, tm1)).to(dev())
+    assert torch.equal(got, want)
+    assert a.getstate() == b.getstate()
+
+
 def test_draw_coeffs_vec_device_path_matches_reference_fixture():
     """draw_coeffs_vec (device MT by default) reproduces the coefficients the
     reference consumed for F1 (tests/golden), and the split from them matches."""

@@ -257,9 +257,11 @@ def test_mt19937_skip_matches_cpython(start_words):
     """dn_mt19937_skip (jump-ahead: Horner of x^J mod P on the 624-word window,
     polynomials from tools/gen_mt_jump.py) lands on exactly the state CPython
     reaches by generating the words — across the head of the current array,
-    block boundaries and several 17*2^16-word jump units."""
-    L = 17 * (1 << 16)
-    for words in (0, 1, 17, 600, 624, 625, 5000, L - 1, L, L + 624, 3 * L + 12345, 7 * L + 1):
+    block boundaries, the first-digit windows (A_0, B_b) and the second digit
+    (A_a, a >= 1: 64 L words and more) of the 17*2^14-word jump units."""
+    L = 17 * (1 << 14)
+    for words in (0, 1, 17, 600, 624, 625, 5000, L - 1, L, L + 624, 3 * L + 12345, 7 * L + 1, 14 * L + 9,
+                  64 * L + 700, 70 * L + 3, 200 * L + 5):
         a = random.Random(99)
         a.getrandbits(32 * start_words) if start_words else None
         b = random.Random()
@@ -272,3 +274,20 @@ def test_mt19937_skip_matches_cpython(start_words):
             left -= take
         assert a.getstate() == b.getstate(), words
         assert a.getrandbits(64) == b.getrandbits(64)
+
+
+def test_mt19937_skip_third_digit_composes():
+    """Skips past 4097 jump units use the third radix-64 digit (C_c): one skip
+    equals the same distance in two skips that stay below it, from two start
+    indices; and it is additive across the C/A/B digit boundaries."""
+    L = 17 * (1 << 14)
+    for start in (0, 311):
+        for total, first in ((4097 * L + 17, 2000 * L + 8), (9000 * L + 5, 4095 * L + 623), (4160 * L, 64 * L)):
+            a = random.Random(7)
+            a.getrandbits(32 * start) if start else None
+            b = random.Random()
+            b.setstate(a.getstate())
+            _native.mt_skip(a, total)
+            _native.mt_skip(b, first)
+            _native.mt_skip(b, total - first)
+            assert a.getstate() == b.getstate(), (start, total, first)

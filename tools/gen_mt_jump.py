@@ -10,10 +10,18 @@ words is then g(f) with g = x^J mod P, evaluated by Horner (Haramoto,
 Matsumoto, Nishimura, Panneton, L'Ecuyer, "Efficient jump ahead for F2-linear
 random number generators", INFORMS J. Computing 20(3), 2008).
 
-Emitted: P is not needed at run time, only g for J = L - 624 and J = 2^k L
-(k = 0..K-1), L = 17 * 2^16 words (whole 521-bit draws of 17 words).
-The script checks every polynomial against plain stepping before writing.
-Run once; the output is committed (~80 KB).
+Emitted: P is not needed at run time, only g for the substream windows of
+the device draw (L = 17 * 2^14 words = 2^14 whole 521-bit draws per substream).
+Window s >= 1 starts L - 624 + (s - 1) L words after the caller's position;
+with s - 1 = 4096 c + 64 a + b (radix-64 digits, c, a, b < 64) it is
+  W(1 + 64 a)               = A_a (W_idx),  A_a = x^(L - 624 + 64 a L), a = 0..63
+  W(1 + 4096 c + 64 a)      = C_c (W(1 + 64 a)),  C_c = x^(4096 c L), c = 1..63
+  W(1 + 4096 c + 64 a + b)  = B_b (W(1 + 4096 c + 64 a)),  B_b = x^(b L), b = 1..63
+so every window is at most three jumps from the caller's window, and all the
+windows of one level are independent (one GPU launch per level).
+The script checks the two smallest polynomials against plain stepping, and
+every product against an independent square-and-multiply.
+Run once; the output is committed (~1.3 MB of hex).
 """
 import os
 import random
@@ -21,8 +29,8 @@ import sys
 
 N, M = 624, 397
 UP, LO, MA = 0x80000000, 0x7FFFFFFF, 0x9908B0DF
-L_WORDS = 17 * (1 << 16)
-K = 12
+L_WORDS = 17 * (1 << 14)
+RADIX = 64
 DEG = 19937
 
 
@@ -74,6 +82,44 @@ def mod(a, P):
     return a
 
 
+def clmul(a, b):
+    """carry-less product, 8-bit windows of b"""
+    tab = [0] * 256
+    for m in range(1, 256):
+        low = m & -m
+        tab[m] = tab[m ^ low] ^ (a << (low.bit_length() - 1))
+    r, sh = 0, 0
+    while b:
+        r ^= tab[b & 0xFF] << sh
+        b >>= 8
+        sh += 8
+    return r
+
+
+class Reducer:
+    """a mod P, eight bits at a time: R[t] clears the top byte t."""
+
+    def __init__(self, P):
+        self.P = P
+        self.d = P.bit_length() - 1
+        self.R = [0] * 256
+        for t in range(256):
+            v, q = t << self.d, 0
+            for i in range(7, -1, -1):
+                if (v >> (self.d + i)) & 1:
+                    v ^= P << i
+                    q |= 1 << i
+            self.R[t] = clmul(P, q)
+
+    def __call__(self, a):
+        d = self.d
+        while a.bit_length() > d + 8:
+            top = a.bit_length() - 8
+            t = a >> top
+            a ^= self.R[t] << (top - d)
+        return mod(a, self.P)
+
+
 def xpow(J, P):
     r = 1
     for b in bin(J)[2:]:
@@ -103,14 +149,29 @@ def main(out_path):
     assert L == DEG, L
     P = int(bin(C)[2:].zfill(L + 1)[::-1], 2)
     assert P.bit_length() - 1 == DEG
-    polys = [("kMtJumpHead", L_WORDS - N, xpow(L_WORDS - N, P))]
-    g = xpow(L_WORDS, P)
-    for k in range(K):
-        polys.append((f"kMtJump{k}", L_WORDS << k, g))
-        g = mod(sq(g), P)
-    # check the two smallest jumps against plain stepping
+    red = Reducer(P)
+    mm = lambda x, y: red(clmul(x, y))  # noqa: E731
+    xL = xpow(L_WORDS, P)
+    x64L = xpow(64 * L_WORDS, P)
+    x4096L = xpow(4096 * L_WORDS, P)
+    polys = []
+    g = xpow(L_WORDS - N, P)
+    for a in range(RADIX):  # A_a = x^(L - 624 + 64 a L)
+        polys.append((f"A{a}", L_WORDS - N + 64 * a * L_WORDS, g))
+        g = mm(g, x64L)
+    g = x4096L
+    for c in range(1, RADIX):  # C_c = x^(4096 c L)
+        polys.append((f"C{c}", 4096 * c * L_WORDS, g))
+        g = mm(g, x4096L)
+    g = xL
+    for b in range(1, RADIX):  # B_b = x^(b L)
+        polys.append((f"B{b}", b * L_WORDS, g))
+        g = mm(g, xL)
+    for name, J, gp in polys[::17]:  # products vs direct square-and-multiply
+        assert gp == xpow(J, P), name
+    # check the two smallest jumps (A_0, B_1) against plain stepping
     w0 = list(random.Random(5).getstate()[1][:N])
-    for name, J, gp in polys[:2]:
+    for name, J, gp in (polys[0], polys[2 * RADIX - 1]):
         a = jump(w0, gp)
         b = w0
         for _ in range(J):
@@ -123,18 +184,25 @@ def main(out_path):
         f.write("// polynomial of MT19937's one-word transition (degree 19937); bit i of word\n")
         f.write("// i/64 is the coefficient of x^i.\n")
         f.write(f"constexpr uint64_t kMtJumpL = {L_WORDS}ull;  // words per device substream\n")
-        f.write(f"constexpr int kMtJumpLevels = {K};\n")
+        f.write(f"constexpr int kMtJumpRadix = {RADIX};\n")
         f.write(f"constexpr int kMtPolyWords = {nw};\n")
-        f.write(f"alignas(64) static const uint64_t kMtJumpPolys[{len(polys)}][{nw}] = {{\n")
+        f.write("// rows: A_a = x^(L - 624 + 64 a L) (a = 0..63) at row a; C_c = x^(4096 c L) (c = 1..63) at\n")
+        f.write("// row 63 + c; B_b = x^(b L) (b = 1..63) at row 126 + b.\n")
+        f.write("constexpr int kMtRowA = 0, kMtRowC = 63, kMtRowB = 126;\n")
+        f.write(f"constexpr int kMtJumpRows = {len(polys)};\n")
+        f.write("// initializer of a [kMtJumpRows][kMtPolyWords] uint64_t array (host and device copies)\n")
+        f.write("#define DN_MT_JUMP_POLYS { \\\n")
         for name, J, gp in polys:
-            f.write(f"  // {name}: J = {J}\n  {{")
+            f.write(f"  /* {name}: J = {J} */ {{ \\")
             ws = [(gp >> (64 * i)) & ((1 << 64) - 1) for i in range(nw)]
             for i, wv in enumerate(ws):
                 if i % 6 == 0:
                     f.write("\n   ")
                 f.write(f" 0x{wv:016x}ull,")
-            f.write("\n  },\n")
-        f.write("};\n")
+                if i % 6 == 5 or i == nw - 1:
+                    f.write(" \\")
+            f.write("\n  }, \\\n")
+        f.write("}\n")
     print("wrote", out_path)
 
 
