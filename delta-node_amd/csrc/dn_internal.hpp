@@ -24,6 +24,19 @@ inline const char* tune_env(const char* name) {
 // Record a thread-local error message and return `code` (printf-style).
 int set_error(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 
+// Forward differences (split by additions) stay below 2^544 while
+// sum_{j<t} (n+t)^j < 2^23 (every table entry and every intermediate Newton
+// coefficient is bounded by f at some x <= n + t - 1); otherwise the split
+// folds after every Horner step.
+inline bool fd_needs_fold(int t, int n) {
+  double s = 0.0, p = 1.0;
+  for (int j = 0; j < t; ++j) {
+    s += p;
+    p *= static_cast<double>(n + t);
+  }
+  return s >= 8388608.0;
+}
+
 // Compute units of the current device (cached per device; shamir_m521.hip).
 int device_cu_count();
 

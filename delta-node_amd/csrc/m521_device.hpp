@@ -214,6 +214,61 @@ __device__ __forceinline__ void mul_small_add(uint32_t v[kLimbs], uint32_t x, co
   mul_small_add(v, v, x, c);
 }
 
+// ---- forward differences (split) -------------------------------------------
+// D = 2 * c (a one-bit left shift across limbs; c < 2^543 so no overflow).
+// D may alias c: limb i reads c[i] and c[i-1] before either is overwritten.
+__device__ __forceinline__ void twice(uint32_t D[kLimbs], const uint32_t c[kLimbs]) {
+#pragma unroll
+  for (int i = kLimbs - 1; i > 0; --i) D[i] = __builtin_amdgcn_alignbit(c[i], c[i - 1], 31);
+  D[0] = c[0] << 1;
+}
+
+constexpr int64_t fd_factorial(int k) { return k <= 1 ? 1 : k * fd_factorial(k - 1); }
+
+// In place, c becomes the forward-difference table of f at x = 1:
+// synthetic division by (x - z) for z = 1..T-1 turns the monomial
+// coefficients into Newton coefficients b_k on nodes 1, 2, ...
+// (f = b0 + b1 (x-1) + b2 (x-1)(x-2) + ...), and Delta^k f(1) = k! b_k.
+// Every step is c[j] += z * c[j+1] with a small constant z.
+template <int T>
+__device__ __forceinline__ void fd_init(uint32_t c[T][kLimbs]) {
+  if constexpr (T == 3) {
+    // hand-ordered for the headline t = 3 (58 VGPRs, 8 waves/SIMD):
+    // D2 = 2 c2; c2 <- c1 + c2; c1 <- c2 + D2 (= c1 + 3 c2); c2 <- c2 + c0.
+    // (c0 is added last: an int64 secret is 2 live limbs until then.)
+    uint32_t d2[kLimbs];
+    twice(d2, c[2]);
+    add_fe(c[2], c[1]);
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) c[1][i] = c[2][i];
+    add_fe(c[1], d2);
+    add_fe(c[2], c[0]);
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) {
+      c[0][i] = c[2][i];
+      c[2][i] = d2[i];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k + 1 < T; ++k) {
+#pragma unroll
+      for (int j = T - 2; j >= k; --j) {
+        if (k == 0) add_fe(c[j], c[j + 1]);
+        else mul_small_add(c[j], c[j + 1], static_cast<uint32_t>(k + 1), c[j]);
+      }
+    }
+    if constexpr (T >= 3) {
+#pragma unroll
+      for (int k = 2; k < T; ++k) {
+        uint32_t zero[kLimbs];
+#pragma unroll
+        for (int i = 0; i < kLimbs; ++i) zero[i] = 0u;
+        mul_small_add(c[k], c[k], static_cast<uint32_t>(fd_factorial(k)), zero);
+      }
+    }
+  }
+}
+
 // ---- wide accumulators (reconstruct) --------------------------------------
 // S[0..N) += a[0..A) * y[0..17)   (schoolbook).  FRESH: S was zero before the
 // call, so limb j+17 is still untouched when row j ends and takes the carry

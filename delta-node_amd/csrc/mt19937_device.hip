@@ -44,11 +44,12 @@ namespace {
 
 __device__ const uint64_t kMtPolysDev[kMtJumpRows][kMtPolyWords] = DN_MT_JUMP_POLYS;
 
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
 constexpr int kMtN = 624, kMtM = 397;
 constexpr uint32_t kMtA = 0x9908b0dfu, kMtUp = 0x80000000u, kMtLo = 0x7fffffffu;
 constexpr uint64_t kCoefPerSub = kMtJumpL / 17;            // 2^14 draws per substream
-constexpr int kGroup = 64 * 17;                            // words of one emission group (64 draws)
-constexpr int kRingG = 2 * kGroup;                         // tempered-word ring of the generation wave
 static_assert(kMtJumpL % 17 == 0, "substreams hold whole 17-word draws");
 
 __host__ __device__ inline uint32_t mt_temper(uint32_t y) {
@@ -85,40 +86,127 @@ struct JumpArgs {
   uint32_t njobs;
 };
 
-constexpr int kERow = 704;  // E row: 16 zero words, then 684 words of a T stream (+4 pad)
+// Jump and generation waves keep a 624-word MT window in registers: Q[11] a
+// 704-slot ring (slot 64 r + lane), the window's word i at slot 16 + i of the
+// current frame.  One append = the next 64 words of the stream
+// (mix(word l, word l + 1, word l + 397), operands by ds_bpermute), written
+// to the frame's free register; the frame then moves by one register.
+// APPEND<K> is append number K mod 11 of an unrolled run: logical register r
+// is Q[(r + K) % 11], so no register moves.
+struct Lanes {
+  int pa, pb, pm;  // ds_bpermute byte addresses of lanes l + 16, l + 17, l + 29 (mod 64)
+  bool la, lb, lm;  // lane < 16, < 17, < 29
+};
 
-// One workgroup = 4 jumps from the same source window W (the host groups
-// them).  Horner over 4-bit chunks of g, 16 chunks (one 64-bit word of g) per
-// step: r <- f^64(r) ^ sum_t f^(4 (15 - t))(T[c_t]), T[v] = sum over bits j of
-// v of f^j(W).  f^m(T[v]) is the window at offset m of T[v]'s own stream, so
-// the workgroup stores those streams once, E[v] = words 0..683 of T[v]'s
-// stream (LDS, 45 KB), and a step is
+template <int K>
+__device__ __forceinline__ uint32_t append64(uint32_t (&Q)[11], const Lanes& L) {
+  const uint32_t xa = static_cast<uint32_t>(
+      __builtin_amdgcn_ds_bpermute(L.pa, static_cast<int>(L.la ? Q[(1 + K) % 11] : Q[K % 11])));
+  const uint32_t xb = static_cast<uint32_t>(
+      __builtin_amdgcn_ds_bpermute(L.pb, static_cast<int>(L.lb ? Q[(1 + K) % 11] : Q[K % 11])));
+  const uint32_t xm = static_cast<uint32_t>(
+      __builtin_amdgcn_ds_bpermute(L.pm, static_cast<int>(L.lm ? Q[(7 + K) % 11] : Q[(6 + K) % 11])));
+  Q[(10 + K) % 11] = mt_mix(xa, xb, xm);
+  return Q[(10 + K) % 11];
+}
+
+// Jump table of one source window W, E[v] = words 0..683 of the stream of
+// T[v] = sum over bits j of v of f^j(W), stored for b128 reads: entry (v, m)
+// is a 28-word row holding E[v][64 k + m - 16] for k = 0..10 (words 0..10)
+// and again for k = 1..10 (words 12..21), zero outside 0..683, so the ten
+// words a lane XORs into its ten window registers for one chunk are one
+// 16-B-aligned run of a row (two ds_read_b128 + one ds_read_b64).  The 28-word
+// pitch spreads a b128 lane group over all 64 banks (a 24-word pitch reads
+// every group 2-way conflicted: 356 vs 252 LDS cycles per 16 chunks).
+constexpr int kEPitch = 28;
+constexpr int kEVWords = 64 * kEPitch;  // words per chunk value v
+constexpr int kJumpWaves = 8;           // jumps (waves) per workgroup, all from one source
+
+// a ^ b ^ c in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96;
+// hipcc keeps two v_xor_b32 otherwise)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// the ten table words of chunk t (value c) for this lane: off = the lane's row offset for t
+__device__ __forceinline__ void table_words(const uint32_t* E, uint32_t off, uint32_t c, uint32_t (&x)[10]) {
+  const uint32_t* p = E + c * kEVWords + off;
+  const u32x4_t a = *reinterpret_cast<const u32x4_t*>(p);
+  const u32x4_t b = *reinterpret_cast<const u32x4_t*>(p + 4);
+  const u32x2_t d = *reinterpret_cast<const u32x2_t*>(p + 8);
+  x[0] = a.x, x[1] = a.y, x[2] = a.z, x[3] = a.w, x[4] = b.x, x[5] = b.y, x[6] = b.z, x[7] = b.w, x[8] = d.x,
+  x[9] = d.y;
+}
+
+// One Horner step over the 64-bit word gw of g in frame K (logical register
+// r is Q[(r + K) % 11]): f^64 into the frame's free register, then the 16
+// table windows XORed (two per instruction) into the 624 window words, which
+// now sit at slots 80 .. 703 of the frame (registers 1 .. 10).
+template <int K>
+__device__ __forceinline__ void jump_mega(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E,
+                                          const uint32_t (&off)[16], uint64_t gw) {
+  // the table reads of chunk pair p + 1 are issued before the XORs of pair p
+  // (f^64's ds_bpermute first: LDS results return in issue order)
+  uint32_t x[2][2][10];
+  append64<K>(Q, L);
+  table_words(E, off[0], static_cast<uint32_t>(gw >> 60) & 15u, x[0][0]);
+  table_words(E, off[1], static_cast<uint32_t>(gw >> 56) & 15u, x[0][1]);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    if (p < 7) {
+      table_words(E, off[2 * p + 2], static_cast<uint32_t>(gw >> (52 - 8 * p)) & 15u, x[(p + 1) & 1][0]);
+      table_words(E, off[2 * p + 3], static_cast<uint32_t>(gw >> (48 - 8 * p)) & 15u, x[(p + 1) & 1][1]);
+    }
+#pragma unroll
+    for (int r = 1; r < 11; ++r)
+      Q[(r + K) % 11] = xor3(Q[(r + K) % 11], x[p & 1][0][r - 1], x[p & 1][1][r - 1]);
+  }
+}
+
+template <int... ks>
+__device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E,
+                                         const uint32_t (&off)[16], const uint64_t* g, int wi,
+                                         std::integer_sequence<int, ks...>) {
+  ((void)[&] {
+     const int w = wi - ks;
+     const uint64_t gw = w < kMtPolyWords ? g[w] : 0ull;
+     jump_mega<ks>(Q, L, E, off, gw);
+   }(),
+   ...);
+}
+
+// One workgroup = up to 8 jumps from the same source window W (the host
+// groups them; padding jobs have dst < 0).  Horner over 4-bit chunks of g,
+// 16 chunks (one 64-bit word of g) per step: r <- f^64(r) ^ sum_t
+// f^(4 (15 - t))(T[c_t]); f^m(T[v]) is the window at offset m of T[v]'s own
+// stream, which the workgroup tables once (E, 96 KB of LDS), so a step is
 //   * f^64(r): 64 new words mix(r[l], r[l+1], r[l+397]), l = 0..63 — one
 //     register, its operands gathered by 3 ds_bpermute;
-//   * the XOR of 16 E windows into the 624 window words (10 registers, 160
-//     LDS reads and XORs per lane).
-// Registers: Q[11] is a 704-slot ring (slot 64 r + lane); at the start of a
-// step word i of r sits at slot 16 + i, the new words land in Q[10] (slots
-// 640..703), and afterwards the frame moves by one register.
-__global__ void __launch_bounds__(256) mt_jump_kernel(const JumpArgs a) {
-  __shared__ uint32_t E[16 * kERow];
+//   * the XOR of 16 table windows into the 624 window words (10 registers;
+//     48 LDS reads and 80 v_bitop3 per lane).
+__global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t E[16 * kEVWords];
   __shared__ uint32_t ext[kMtN + 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  const uint32_t j0 = blockIdx.x * 4u;
+  const uint32_t j0 = blockIdx.x * kJumpWaves;
   const JumpJob* jp = a.jobs + __builtin_amdgcn_readfirstlane(j0 + wid < a.njobs ? j0 + wid : j0);
   const int32_t poly = __builtin_amdgcn_readfirstlane(jp->poly), dsti = __builtin_amdgcn_readfirstlane(jp->dst);
   const uint32_t* src = a.wins + static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(a.jobs[j0].src)) * kMtN;
   // the source stream: words 0..623 of W, then 63 more (each from words <= 459 of W)
-  for (uint32_t i = tid; i < kMtN; i += 256u) ext[i] = src[i];
+  for (uint32_t i = tid; i < kMtN; i += 64u * kJumpWaves) ext[i] = src[i];
   __syncthreads();
   if (tid < 63u) ext[kMtN + tid] = mt_mix(ext[tid], ext[tid + 1], ext[tid + kMtM]);
   __syncthreads();
-  for (uint32_t e = tid; e < 16u * kERow; e += 256u) {
-    const uint32_t v = e / kERow, i = e - v * kERow;
+  for (uint32_t e = tid; e < 16u * kEVWords; e += 64u * kJumpWaves) {
+    const uint32_t v = e / kEVWords, rem = e - v * kEVWords, m = rem / kEPitch, k = rem - m * kEPitch;
+    const int kk = k < 11u ? static_cast<int>(k) : (k >= 12u && k < 22u ? static_cast<int>(k) - 11 : -1);
+    const int j = 64 * kk + static_cast<int>(m) - 16;  // T-stream word
     uint32_t x = 0u;
-    if (i >= 16u && i < 16u + 684u) {
+    if (kk >= 0 && j >= 0 && j < 684) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) x ^= ext[i - 16u + j] & (0u - ((v >> j) & 1u));
+      for (int b = 0; b < 4; ++b) x ^= ext[j + b] & (0u - ((v >> b) & 1u));
     }
     E[e] = x;
   }
@@ -129,33 +217,24 @@ __global__ void __launch_bounds__(256) mt_jump_kernel(const JumpArgs a) {
   uint32_t Q[11];
 #pragma unroll
   for (int r = 0; r < 11; ++r) Q[r] = 0u;
-  // ds_bpermute byte addresses: lane (l + 16), (l + 17), (l + 29) mod 64
-  const int pa = static_cast<int>(((lane + 16u) & 63u) * 4u), pb = static_cast<int>(((lane + 17u) & 63u) * 4u),
-            pm = static_cast<int>(((lane + 29u) & 63u) * 4u);
-  const uint32_t* El = E + lane;
+  Lanes L;
+  L.pa = static_cast<int>(((lane + 16u) & 63u) * 4u);
+  L.pb = static_cast<int>(((lane + 17u) & 63u) * 4u);
+  L.pm = static_cast<int>(((lane + 29u) & 63u) * 4u);
+  L.la = lane < 16u, L.lb = lane < 17u, L.lm = lane < 29u;
+  // chunk t's words for register r (1..10): table index 64 (r - 1) + lane + 60 - 4 t
+  uint32_t off[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const uint32_t u = lane + 60u - 4u * t;
+    off[t] = (u & 63u) * kEPitch + (u >> 6) * 12u;
+  }
   int top = kMtPolyWords - 1;
   while (top > 0 && g[top] == 0ull) --top;  // steps above it leave r = 0
-#pragma unroll 1
-  for (int wi = top; wi >= 0; --wi) {
-    const uint64_t gw = g[wi];
-    // f^64: word l at slot 16 + l, word l + 1 at 17 + l, word l + 397 at 413 + l
-    const uint32_t xa = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(pa, static_cast<int>(lane < 16u ? Q[1] : Q[0])));
-    const uint32_t xb = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(pb, static_cast<int>(lane < 17u ? Q[1] : Q[0])));
-    const uint32_t xm = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(pm, static_cast<int>(lane < 29u ? Q[7] : Q[6])));
-    Q[10] = mt_mix(xa, xb, xm);
-    // new word i (old stream word 64 + i) sits at slot 80 + i: XOR E[c_t][16 + 4 (15 - t) + i]
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const uint32_t c = static_cast<uint32_t>(gw >> (60 - 4 * t)) & 15u;
-      const uint32_t* Ec = El + c * kERow + (60 - 4 * t);
-#pragma unroll
-      for (int r = 1; r < 11; ++r) Q[r] ^= Ec[64 * (r - 1)];
-    }
-    const uint32_t q0 = Q[0];
-#pragma unroll
-    for (int r = 0; r < 10; ++r) Q[r] = Q[r + 1];
-    Q[10] = q0;
-  }
+  // runs of 11 steps (the frame returns to Q[0] after 11); r = 0 before the
+  // first nonzero word, so the run starts with zero words above it
+  for (int wi = top + (10 - top % 11); wi >= 0; wi -= 11)
+    jump_run(Q, L, E, off, g, wi, std::make_integer_sequence<int, 11>{});
   uint32_t* dst = a.wins + static_cast<uint64_t>(dsti) * kMtN;
 #pragma unroll
   for (int r = 0; r < 11; ++r) {
@@ -178,38 +257,20 @@ struct GenArgs {
   int32_t final_sig;     // window the final-state wave starts from (-1: no such wave)
   uint64_t final_pos;    // position of that window's first word (0: the caller's array)
   uint64_t final_tf;     // position of CPython's final array
+  // fused split (mt_gen_kernel<T>, T > 0): int64 secrets in, n share vectors out
+  const int64_t* secrets;
+  uint8_t* shares;
+  uint64_t n_elem;
+  int32_t n_shares;
+  uint32_t ring;         // ring words of one wave (2 emission groups)
 };
-
-// The generation wave keeps the MT stream in registers exactly as a jump
-// wave keeps r: Q[11] a 704-slot ring, the window's word i at slot 16 + i
-// of the current frame.  One append = the next 64 words of the stream
-// (mix(word l, word l + 1, word l + 397), operands by ds_bpermute), written
-// to the frame's free register; the frame then moves by one register.
-// APPEND<K> is append number K mod 11 of an unrolled run: logical register r
-// is Q[(r + K) % 11], so no register moves.
-struct Lanes {
-  int pa, pb, pm;  // ds_bpermute byte addresses of lanes l + 16, l + 17, l + 29 (mod 64)
-  bool la, lb, lm;  // lane < 16, < 17, < 29
-};
-
-template <int K>
-__device__ __forceinline__ uint32_t append64(uint32_t (&Q)[11], const Lanes& L) {
-  const uint32_t xa = static_cast<uint32_t>(
-      __builtin_amdgcn_ds_bpermute(L.pa, static_cast<int>(L.la ? Q[(1 + K) % 11] : Q[K % 11])));
-  const uint32_t xb = static_cast<uint32_t>(
-      __builtin_amdgcn_ds_bpermute(L.pb, static_cast<int>(L.lb ? Q[(1 + K) % 11] : Q[K % 11])));
-  const uint32_t xm = static_cast<uint32_t>(
-      __builtin_amdgcn_ds_bpermute(L.pm, static_cast<int>(L.lm ? Q[(7 + K) % 11] : Q[(6 + K) % 11])));
-  Q[(10 + K) % 11] = mt_mix(xa, xb, xm);
-  return Q[(10 + K) % 11];
-}
 
 // 64 draws of one group (lane = draw c of this substream, words 17 c .. 17 c +
 // 16 of the ring at `rb` words): +1, rejection test, tiled store.
 __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb, uint64_t qb, uint32_t rbm,
                                           uint32_t c, uint32_t nloc, uint32_t lane) {
   if (c >= nloc) return;
-  uint32_t v[kLimbs];
+  uint32_t v[kLimbs];  // (the group's ring slice is 64 draws of 17 words)
   const uint32_t* w = rb + 17u * lane;
 #pragma unroll
   for (int i = 0; i < kLimbs; ++i) v[i] = w[i];
@@ -234,17 +295,55 @@ __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb,
 }
 
 template <int... ks>
-__device__ __forceinline__ void gen_run(uint32_t (&Q)[11], const Lanes& L, uint32_t* R, uint32_t& wpos,
+__device__ __forceinline__ void gen_run(uint32_t (&Q)[11], const Lanes& L, uint32_t* R, uint32_t ring, uint32_t& wpos,
                                         std::integer_sequence<int, ks...>) {
   // each append: temper the 64 new words into the ring at stream word wpos
   ((void)[&] {
      const uint32_t t = mt_temper(append64<ks>(Q, L));
      uint32_t pos = wpos + (threadIdx.x & 63u);
-     pos = pos >= static_cast<uint32_t>(kRingG) ? pos - kRingG : pos;
+     pos = pos >= ring ? pos - ring : pos;
      R[pos] = t;
-     wpos = wpos + 64u >= static_cast<uint32_t>(kRingG) ? wpos + 64u - kRingG : wpos + 64u;
+     wpos = wpos + 64u >= ring ? wpos + 64u - ring : wpos + 64u;
    }(),
    ...);
+}
+
+// Fused split (T = t): the 64 elements of one group (lane = element, 64 (t-1)
+// consecutive draws of this substream, element-major as make_shares draws
+// them: words 17 ((t-1) lane + j - 1) .. + 16 of the group for coefficient j),
+// their int64 secrets, and the split of split_kernel<T, false, false>: the
+// forward-difference table stored share by share.
+template <int T>
+__device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t e, uint32_t lane) {
+  constexpr int TM1 = T - 1;
+  if (e >= a.n_elem) return;
+  uint32_t c[T][kLimbs];
+  const uint32_t* w = rb + 17u * TM1 * lane;
+#pragma unroll
+  for (int j = 1; j < T; ++j) {
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) c[j][i] = w[17 * (j - 1) + i];
+    c[j][16] >>= 23;
+    uint32_t all = c[j][1];
+#pragma unroll
+    for (int i = 2; i < 16; ++i) all &= c[j][i];
+    if (c[j][16] == 0x1FFu && c[j][0] >= 0xFFFFFFFEu && all == 0xFFFFFFFFu) atomicOr(a.flag, 1u);
+    uint32_t cy = 1u;  // randint(1, p-1) = 1 + getrandbits(521)
+#pragma unroll
+    for (int i = 0; i < kLimbs; ++i) c[j][i] = __builtin_addc(c[j][i], 0u, cy, &cy);
+  }
+  const uint64_t s = static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + e));
+  c[0][0] = static_cast<uint32_t>(s);
+  c[0][1] = static_cast<uint32_t>(s >> 32);
+#pragma unroll
+  for (int i = 2; i < kLimbs; ++i) c[0][i] = 0u;
+  fd_init<T>(c);
+  const uint32_t tile = static_cast<uint32_t>(e >> 8), wl = static_cast<uint32_t>(e & 255u);
+#pragma unroll 1
+  for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+    store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vb, tile)), wl, c[0]);
+    fd_step<T>(c);
+  }
 }
 
 template <int... ks>
@@ -259,10 +358,14 @@ __device__ __forceinline__ void final_run(uint32_t (&Q)[11], const Lanes& L, uin
    ...);
 }
 
-__global__ void __launch_bounds__(256) mt_gen_kernel(const GenArgs a) {
-  __shared__ uint32_t s_ring[4][kRingG];
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  const uint32_t sub = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wid);
+// One 64-thread workgroup per substream (one extra for CPython's final state):
+// T == 0 stores the coefficients (groups of 64 draws), T > 0 splits the
+// substream's elements (groups of 64 elements) with them as they are drawn.
+template <int T>
+__global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
+  extern __shared__ uint32_t s_ring[];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t sub = blockIdx.x;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
   const bool fin_wave = sub == a.S;
   const uint32_t wsel = fin_wave ? static_cast<uint32_t>(a.final_sig) : sub;
@@ -288,10 +391,12 @@ __global__ void __launch_bounds__(256) mt_gen_kernel(const GenArgs a) {
     while (np < tf + kMtN) final_run(Q, L, np, tf, a.fin, run11);
     return;
   }
-  uint32_t* R = s_ring[wid];
+  uint32_t* R = s_ring;
+  const uint32_t group = a.ring / 2u;                            // words per emission group
   const uint64_t k0 = static_cast<uint64_t>(sub) * kCoefPerSub;  // first draw of this substream
   const uint32_t nloc = static_cast<uint32_t>(a.ncoef - k0 < kCoefPerSub ? a.ncoef - k0 : kCoefPerSub);
-  const uint32_t ngroups = (nloc + 63u) / 64u;
+  const uint32_t gdraws = T ? 64u * (T - 1) : 64u;  // draws per group
+  const uint32_t ngroups = (nloc + gdraws - 1u) / gdraws;
   const uint64_t qb = k0 / static_cast<uint64_t>(a.tm1);
   const uint32_t rbm = static_cast<uint32_t>(k0 - qb * static_cast<uint64_t>(a.tm1));
   uint32_t wpos = 0;  // ring position of the next stream word of this substream
@@ -302,11 +407,16 @@ __global__ void __launch_bounds__(256) mt_gen_kernel(const GenArgs a) {
   }
   uint32_t done = 0, have = wpos;  // groups emitted, stream words produced
   while (done < ngroups) {
-    gen_run(Q, L, R, wpos, run11);
+    gen_run(Q, L, R, a.ring, wpos, run11);
     have += 11u * 64u;
     wave_sync();
-    while (done < ngroups && have >= (done + 1u) * static_cast<uint32_t>(kGroup)) {
-      emit_group(a, R + (done & 1u) * kGroup, qb, rbm, 64u * done + lane, nloc, lane);
+    while (done < ngroups && have >= (done + 1u) * group) {
+      const uint32_t* rb = R + (done & 1u) * group;
+      if constexpr (T == 0) {
+        emit_group(a, rb, qb, rbm, 64u * done + lane, nloc, lane);
+      } else {
+        emit_split<T>(a, rb, qb + 64u * done + lane, lane);  // k0 / (t-1) = the substream's first element
+      }
       ++done;
     }
     wave_sync();
@@ -315,10 +425,19 @@ __global__ void __launch_bounds__(256) mt_gen_kernel(const GenArgs a) {
 
 uint64_t mt_subs(uint64_t ncoef) { return (ncoef + kCoefPerSub - 1) / kCoefPerSub; }
 
-// Jump jobs of one level, grouped by source window in fours (padding: dst -1).
+// Jump jobs of one level, grouped by source window in workgroups of
+// kJumpWaves jobs (padding: dst -1).
 void push_group(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd) {
   for (size_t i = 0; i < pd.size(); ++i) jobs.push_back({src, pd[i].first, pd[i].second, 0});
-  while (jobs.size() % 4) jobs.push_back({src, 0, -1, 0});
+  while (jobs.size() % kJumpWaves) jobs.push_back({src, 0, -1, 0});
+}
+
+// split a source's jobs into groups of at most `per` (fewer jumps per
+// workgroup = less LDS traffic per CU: the first level is latency-bound)
+void push_groups(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd,
+                 size_t per) {
+  for (size_t i = 0; i < pd.size(); i += per)
+    push_group(jobs, src, std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + per)));
 }
 
 // Levels for windows 1 .. S-1 (s - 1 = 4096 c + 64 a + b; row S holds W_idx):
@@ -332,29 +451,24 @@ void build_levels(uint64_t S, std::vector<JumpJob> lv[3]) {
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t a = 0; a <= last / R && a < R; ++a)
       pd.push_back({kMtRowA + static_cast<int32_t>(a), static_cast<int32_t>(1 + R * a)});
-    for (size_t i = 0; i < pd.size(); i += 4)
-      push_group(lv[0], static_cast<int32_t>(S),
-                 std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + 4)));
+    push_groups(lv[0], static_cast<int32_t>(S), pd, 2);
   }
   for (uint64_t a = 0; a < R && R * a <= last; ++a) {  // C: per source W(1 + 64 a), its c digits
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t c = 1; c < R && R * R * c + R * a <= last; ++c)
       pd.push_back({kMtRowC + static_cast<int32_t>(c), static_cast<int32_t>(1 + R * R * c + R * a)});
-    for (size_t i = 0; i < pd.size(); i += 4)
-      push_group(lv[1], static_cast<int32_t>(1 + R * a),
-                 std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + 4)));
+    push_groups(lv[1], static_cast<int32_t>(1 + R * a), pd, 2);
   }
   for (uint64_t base = 0; base <= last; base += R) {  // B: per source W(1 + base)
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t b = 1; b < R && base + b <= last; ++b)
       pd.push_back({kMtRowB + static_cast<int32_t>(b), static_cast<int32_t>(1 + base + b)});
-    for (size_t i = 0; i < pd.size(); i += 4)
-      push_group(lv[2], static_cast<int32_t>(1 + base),
-                 std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + 4)));
+    push_groups(lv[2], static_cast<int32_t>(1 + base), pd, kJumpWaves);
   }
 }
 
-uint64_t jobs_cap(uint64_t S) { return 2 * S + 1024; }  // >= the three levels with padding
+// >= the three levels with padding (levels A and C: 2 jobs per workgroup of 8)
+uint64_t jobs_cap(uint64_t S) { return 2 * S + 4 * 64 * kJumpWaves + 1024; }
 
 constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
 
@@ -368,22 +482,27 @@ extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
   return kHead + (S + 1) * kMtN * 4 + jobs_cap(S) * sizeof(JumpJob);
 }
 
-extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1,
-                                             void* coeffs, void* scratch, uint64_t scratch_bytes, void* stream) {
-  if (!mt_state || !mt_index) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
-  if (tm1 < 0 || tm1 >= DN_MAX_THRESHOLD)
-    return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: t-1=%d", tm1);
+namespace dn {
+namespace {
+
+// The device draw of n_elem * tm1 coefficients from CPython state
+// (mt_state, *mt_index): jump levels, then `launch_gen(ga, S)` (the
+// generation kernel: coefficients or fused split), then CPython's final state.
+template <typename F>
+int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1, void* scratch,
+                  uint64_t scratch_bytes, void* stream, F launch_gen) {
+  if (!mt_state || !mt_index) return set_error(DN_ERR_ARG, "%s: null pointer", name);
+  if (tm1 < 0 || tm1 >= DN_MAX_THRESHOLD) return set_error(DN_ERR_ARG, "%s: t-1=%d", name, tm1);
   const int32_t idx = *mt_index;
-  if (idx < 0 || idx > kMtN) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: bad MT index");
+  if (idx < 0 || idx > kMtN) return set_error(DN_ERR_ARG, "%s: bad MT index", name);
   const uint64_t ncoef = n_elem * static_cast<uint64_t>(tm1);
   if (ncoef == 0) return DN_OK;
-  if (!coeffs || !scratch) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
+  if (!scratch) return set_error(DN_ERR_ARG, "%s: null pointer", name);
   const uint64_t S = mt_subs(ncoef);
   if (S > mt_jump_max_subs() - 1)
-    return set_error(DN_ERR_UNSUPPORTED, "dn_mt19937_draw_coeffs_device: %llu words exceed the jump table",
+    return set_error(DN_ERR_UNSUPPORTED, "%s: %llu words exceed the jump table", name,
                      static_cast<unsigned long long>(17 * ncoef));
-  if (scratch_bytes < dn_mt19937_device_scratch_bytes(n_elem, tm1))
-    return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: scratch too small");
+  if (scratch_bytes < dn_mt19937_device_scratch_bytes(n_elem, tm1)) return set_error(DN_ERR_ARG, "%s: scratch too small", name);
 
   // CPython's state after the draw: the array at buffer position tf = 624 q,
   // stepped by the final-state wave from window `sig` (position P_sig < tf)
@@ -392,62 +511,117 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
   uint64_t fpos = 0, ftf = 0;
   if (words > h) {
     const uint64_t m_end = words - h, q = (m_end + kMtN - 1) / kMtN, tf = kMtN * q;
-    uint64_t s = (tf + kMtN - 1 - static_cast<uint64_t>(idx)) / kMtJumpL;  // idx + s L - 624 < tf
-    if (s > S - 1) s = S - 1;
-    sig = static_cast<int32_t>(s);
-    fpos = s ? static_cast<uint64_t>(idx) + s * kMtJumpL - kMtN : 0;
+    uint64_t sg = (tf + kMtN - 1 - static_cast<uint64_t>(idx)) / kMtJumpL;  // idx + sg L - 624 < tf
+    if (sg > S - 1) sg = S - 1;
+    sig = static_cast<int32_t>(sg);
+    fpos = sg ? static_cast<uint64_t>(idx) + sg * kMtJumpL - kMtN : 0;
     ftf = tf;
     fidx = static_cast<int32_t>(m_end - kMtN * (q - 1));
   }
 
-  // host staging: window 0 = the caller's array, row S = it advanced idx words; the jump jobs
+  // scratch: head (flag at 0, final array at 256) | windows 0..S (row 0 the
+  // caller's array, row S that array advanced idx words) | jump jobs.  Two
+  // copies: [zeroed head, row 0] and [row S, jobs].
   std::vector<JumpJob> lv[3];
   build_levels(S, lv);
   const uint64_t njobs = lv[0].size() + lv[1].size() + lv[2].size();
-  if (njobs > jobs_cap(S)) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: job table overflow");
-  std::vector<uint32_t> w_idx(kMtN);
-  mt_advance_window(mt_state, static_cast<uint64_t>(idx), w_idx.data());
-
+  if (njobs > jobs_cap(S)) return set_error(DN_ERR_ARG, "%s: job table overflow", name);
+  std::vector<uint32_t> st1(kHead / 4 + kMtN, 0u);
+  std::memcpy(st1.data() + kHead / 4, mt_state, kMtN * 4);
+  std::vector<uint32_t> st2(kMtN + njobs * sizeof(JumpJob) / 4);
+  mt_advance_window(mt_state, static_cast<uint64_t>(idx), st2.data());
+  {
+    uint64_t o = kMtN;
+    for (auto& l : lv) {
+      std::memcpy(st2.data() + o, l.data(), l.size() * sizeof(JumpJob));
+      o += l.size() * sizeof(JumpJob) / 4;
+    }
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
-  uint32_t* flag = reinterpret_cast<uint32_t*>(sc);
-  uint32_t* fin = reinterpret_cast<uint32_t*>(sc + 256);
   uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead);
   JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead + (S + 1) * kMtN * 4);
-  std::vector<JumpJob> all;
-  all.reserve(njobs);
-  for (auto& l : lv) all.insert(all.end(), l.begin(), l.end());
-  hipError_t err = hipMemsetAsync(flag, 0, 4, s);
-  if (err == hipSuccess) err = hipMemcpyAsync(dwin, mt_state, kMtN * 4, hipMemcpyHostToDevice, s);
-  if (err == hipSuccess) err = hipMemcpyAsync(dwin + S * kMtN, w_idx.data(), kMtN * 4, hipMemcpyHostToDevice, s);
-  if (err == hipSuccess && njobs)
-    err = hipMemcpyAsync(djobs, all.data(), njobs * sizeof(JumpJob), hipMemcpyHostToDevice, s);
-  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: %s", hipGetErrorString(err));
+  hipError_t err = hipMemcpyAsync(sc, st1.data(), st1.size() * 4, hipMemcpyHostToDevice, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(dwin + S * kMtN, st2.data(), st2.size() * 4, hipMemcpyHostToDevice, s);
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   uint64_t off = 0;
   for (auto& l : lv) {
     if (!l.empty()) {
       const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.size())};
-      hipLaunchKernelGGL(mt_jump_kernel, dim3(static_cast<uint32_t>(l.size() / 4)), dim3(256), 0, s, ja);
+      hipLaunchKernelGGL(mt_jump_kernel, dim3(static_cast<uint32_t>(l.size() / kJumpWaves)), dim3(64 * kJumpWaves), 0, s,
+                         ja);
     }
     off += l.size();
   }
-  GenArgs ga{dwin, static_cast<uint8_t*>(coeffs), flag, fin, ncoef, dn_m521_vec_bytes(n_elem),
-             ((1ull << 32) + static_cast<uint64_t>(tm1) - 1) / static_cast<uint64_t>(tm1), static_cast<uint32_t>(S),
-             static_cast<uint32_t>(idx), tm1, sig, fpos, ftf};
-  hipLaunchKernelGGL(mt_gen_kernel, dim3(static_cast<uint32_t>((S + 1 + 3) / 4)), dim3(256), 0, s, ga);
+  GenArgs ga{};
+  ga.wins = dwin;
+  ga.flag = reinterpret_cast<uint32_t*>(sc);
+  ga.fin = reinterpret_cast<uint32_t*>(sc + 256);
+  ga.ncoef = ncoef;
+  ga.vb = dn_m521_vec_bytes(n_elem);
+  ga.tm1_magic = ((1ull << 32) + static_cast<uint64_t>(tm1) - 1) / static_cast<uint64_t>(tm1);
+  ga.S = static_cast<uint32_t>(S);
+  ga.idx = static_cast<uint32_t>(idx);
+  ga.tm1 = tm1;
+  ga.final_sig = sig;
+  ga.final_pos = fpos;
+  ga.final_tf = ftf;
+  ga.n_elem = n_elem;
+  launch_gen(ga, s);
   err = hipGetLastError();
-  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: launch: %s", hipGetErrorString(err));
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: launch: %s", name, hipGetErrorString(err));
 
   std::vector<uint32_t> head(256 / 4 + kMtN);  // flag .. final array
   err = hipMemcpyAsync(head.data(), sc, head.size() * 4, hipMemcpyDeviceToHost, s);
   if (err == hipSuccess) err = hipStreamSynchronize(s);
-  if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_draw_coeffs_device: %s", hipGetErrorString(err));
+  if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   // DN_MT_FORCE_RETRY=1 (tuning build) takes the rejected-draw exit so the
   // caller's host fallback can be exercised.
   const char* fr = tune_env("DN_MT_FORCE_RETRY");
-  if (head[0] || (fr && fr[0] == '1'))
-    return set_error(DN_ERR_RETRY, "dn_mt19937_draw_coeffs_device: a draw was rejected; redo on the host");
+  if (head[0] || (fr && fr[0] == '1')) return set_error(DN_ERR_RETRY, "%s: a draw was rejected; redo on the host", name);
   if (sig >= 0) std::memcpy(mt_state, head.data() + 256 / 4, kMtN * 4);
   *mt_index = fidx;
   return DN_OK;
+}
+
+template <int T>
+void launch_gen(GenArgs& ga, hipStream_t s) {
+  ga.ring = 2u * 17u * 64u * (T ? T - 1 : 1);
+  hipLaunchKernelGGL((mt_gen_kernel<T>), dim3(ga.S + 1), dim3(64), ga.ring * 4u, s, ga);
+}
+
+}  // namespace
+}  // namespace dn
+
+extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1,
+                                             void* coeffs, void* scratch, uint64_t scratch_bytes, void* stream) {
+  if (n_elem && tm1 > 0 && !coeffs) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
+  return mt_device_run("dn_mt19937_draw_coeffs_device", mt_state, mt_index, n_elem, tm1, scratch, scratch_bytes, stream,
+                       [&](GenArgs& ga, hipStream_t s) {
+                         ga.coeffs = static_cast<uint8_t*>(coeffs);
+                         launch_gen<0>(ga, s);
+                       });
+}
+
+extern "C" int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, const int64_t* secrets, void* shares,
+                                       uint64_t n_elem, int threshold, int n_shares, void* scratch,
+                                       uint64_t scratch_bytes, void* stream) {
+  const char* name = "dn_mt19937_split_device";
+  if (threshold < 1 || threshold > DN_MAX_THRESHOLD)
+    return set_error(DN_ERR_UNSUPPORTED, "%s: threshold %d outside 1..%d", name, threshold, DN_MAX_THRESHOLD);
+  if (threshold > n_shares) return set_error(DN_ERR_THRESHOLD, "threshold should be little equal than shares");
+  if (!(threshold == 2 || threshold == 3 || threshold == 5) || fd_needs_fold(threshold, n_shares) ||
+      n_shares > DN_MAX_SHARES)
+    return set_error(DN_ERR_UNSUPPORTED, "%s: fused form needs t in {2, 3, 5} and forward differences (t=%d, n=%d)",
+                     name, threshold, n_shares);
+  if (n_elem && (!secrets || !shares)) return set_error(DN_ERR_ARG, "%s: null pointer", name);
+  return mt_device_run(name, mt_state, mt_index, n_elem, threshold - 1, scratch, scratch_bytes, stream,
+                       [&](GenArgs& ga, hipStream_t s) {
+                         ga.secrets = secrets;
+                         ga.shares = static_cast<uint8_t*>(shares);
+                         ga.n_shares = n_shares;
+                         if (threshold == 2) launch_gen<2>(ga, s);
+                         else if (threshold == 3) launch_gen<3>(ga, s);
+                         else launch_gen<5>(ga, s);
+                       });
 }

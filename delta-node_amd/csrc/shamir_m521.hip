@@ -103,15 +103,6 @@ __device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, u
   }
 }
 
-// D = 2 * c (a one-bit left shift across limbs; c < 2^543 so no overflow).
-// D may alias c: limb i reads c[i] and c[i-1] before either is overwritten.
-__device__ __forceinline__ void twice(uint32_t D[kLimbs], const uint32_t c[kLimbs]) {
-#pragma unroll
-  for (int i = kLimbs - 1; i > 0; --i) D[i] = __builtin_amdgcn_alignbit(c[i], c[i - 1], 31);
-  D[0] = c[0] << 1;
-}
-
-constexpr int64_t fd_factorial(int k) { return k <= 1 ? 1 : k * fd_factorial(k - 1); }
 
 // T = compile-time threshold (1..8).
 // FOLD == false: f(x) for x = 1..n by forward differences — the table
@@ -155,50 +146,6 @@ __device__ __forceinline__ void prng_coeffs_of(const SplitArgs& a, uint32_t tile
     c[j][16] = tops[w * (T - 1) + (j - 1)] & kTopMask;
     if (__builtin_expect(prng_rejected(c[j]), 0)) prng_retry(c[j], a.key, i);
     add_small(c[j], 1u);
-  }
-}
-
-// In place, c becomes the forward-difference table of f at x = 1:
-// synthetic division by (x - z) for z = 1..T-1 turns the monomial
-// coefficients into Newton coefficients b_k on nodes 1, 2, ...
-// (f = b0 + b1 (x-1) + b2 (x-1)(x-2) + ...), and Delta^k f(1) = k! b_k.
-// Every step is c[j] += z * c[j+1] with a small constant z.
-template <int T>
-__device__ __forceinline__ void fd_init(uint32_t c[T][kLimbs]) {
-  if constexpr (T == 3) {
-    // hand-ordered for the headline t = 3 (58 VGPRs, 8 waves/SIMD):
-    // D2 = 2 c2; c2 <- c1 + c2; c1 <- c2 + D2 (= c1 + 3 c2); c2 <- c2 + c0.
-    // (c0 is added last: an int64 secret is 2 live limbs until then.)
-    uint32_t d2[kLimbs];
-    twice(d2, c[2]);
-    add_fe(c[2], c[1]);
-#pragma unroll
-    for (int i = 0; i < kLimbs; ++i) c[1][i] = c[2][i];
-    add_fe(c[1], d2);
-    add_fe(c[2], c[0]);
-#pragma unroll
-    for (int i = 0; i < kLimbs; ++i) {
-      c[0][i] = c[2][i];
-      c[2][i] = d2[i];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k + 1 < T; ++k) {
-#pragma unroll
-      for (int j = T - 2; j >= k; --j) {
-        if (k == 0) add_fe(c[j], c[j + 1]);
-        else mul_small_add(c[j], c[j + 1], static_cast<uint32_t>(k + 1), c[j]);
-      }
-    }
-    if constexpr (T >= 3) {
-#pragma unroll
-      for (int k = 2; k < T; ++k) {
-        uint32_t zero[kLimbs];
-#pragma unroll
-        for (int i = 0; i < kLimbs; ++i) zero[i] = 0u;
-        mul_small_add(c[k], c[k], static_cast<uint32_t>(fd_factorial(k)), zero);
-      }
-    }
   }
 }
 
@@ -634,18 +581,6 @@ static int check_launch(const char* what) {
   return DN_OK;
 }
 
-// Forward differences stay below 2^544 while sum_{j<t} (n+t)^j < 2^23
-// (every table entry, and every intermediate Newton coefficient, is bounded by
-// f at some x <= n + t - 1); otherwise fold.
-static bool needs_fold(int t, int n) {
-  double s = 0.0, p = 1.0;
-  for (int j = 0; j < t; ++j) {
-    s += p;
-    p *= static_cast<double>(n + t);
-  }
-  return s >= 8388608.0;
-}
-
 template <bool FE_SECRET, bool FOLD>
 static void launch_split_t(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
   switch (t) {
@@ -762,7 +697,7 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   a.threshold = threshold;
   // DN_SPLIT_HORNER=1 forces the Horner kernel (A/B hook, read per call).
   const char* hz = tune_env("DN_SPLIT_HORNER");
-  const bool fold_each = needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
+  const bool fold_each = fd_needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
   const bool per_cu = !prng && !fold_each && threshold <= 8;  // the memory-bound difference-table kernels
   const dim3 g(grid_for(a.ntiles, per_cu));
   a.tile_map = tile_map_for(static_cast<int>(g.x), !prng);

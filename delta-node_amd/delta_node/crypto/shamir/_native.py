@@ -41,6 +41,7 @@ EXPORTS = (
     "dn_m521_reconstruct", "dn_mt19937_draw_coeffs", "dn_last_error", "dn_version",
     "dn_m521_split_prng", "dn_m521_prng_coeffs",
     "dn_mt19937_device_scratch_bytes", "dn_mt19937_draw_coeffs_device", "dn_mt19937_skip",
+    "dn_mt19937_split_device",
 )
 
 
@@ -134,6 +135,9 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_mt19937_draw_coeffs_device.restype = i32
     L.dn_mt19937_draw_coeffs_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
                                                 u64, i32, vp, vp, u64, vp]
+    L.dn_mt19937_split_device.restype = i32
+    L.dn_mt19937_split_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), vp, vp, u64,
+                                          i32, i32, vp, u64, vp]
     L.dn_mt19937_skip.restype = i32
     L.dn_mt19937_skip.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64]
     L.dn_last_error.restype = ctypes.c_char_p
@@ -295,6 +299,29 @@ def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
     version, gauss, state, index = _mt_state(rng)
     rc = L.dn_mt19937_draw_coeffs_device(state, ctypes.byref(index), n, tm1, out.data_ptr(), scratch.data_ptr(), sb,
                                          stream_ptr())
+    if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
+        return False
+    check(rc)
+    rng.setstate((version, tuple(state) + (index.value,), gauss))
+    return True
+
+
+def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool:
+    """make_shares over n int64 secrets with coefficients drawn from `rng`
+    (a random.Random) as n sequential make_shares calls would, draw and split
+    fused on the GPU (dn_mt19937_split_device) into `shares` (uint8 device
+    [n_shares, vec_bytes(n)]).  False (rng untouched, shares unspecified) when
+    the fused form does not apply or a draw was rejected: draw, then split."""
+    import torch
+
+    if n == 0:
+        return True
+    L = lib()
+    sb = int(L.dn_mt19937_device_scratch_bytes(n, t - 1))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=shares.device)
+    version, gauss, state, index = _mt_state(rng)
+    rc = L.dn_mt19937_split_device(state, ctypes.byref(index), secrets.data_ptr(), shares.data_ptr(), n, t, n_shares,
+                                   scratch.data_ptr(), sb, stream_ptr())
     if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
         return False
     check(rc)

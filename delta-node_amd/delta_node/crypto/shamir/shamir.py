@@ -29,7 +29,6 @@ call raises.  Only the default prime (the Mersenne prime M521) is supported;
 """
 from __future__ import annotations
 
-import os
 import random
 from functools import reduce
 from typing import List, Optional, Sequence, Tuple, Union
@@ -221,7 +220,7 @@ class SecretShare(object):
             rng = self.random
         self.last_draw_rejected = False
         blk = None
-        if tm1 > 0 and n > 0 and torch.device(dev).type == "cuda" and os.environ.get("DN_MT_DEVICE", "1") != "0":
+        if tm1 > 0 and n > 0 and torch.device(dev).type == "cuda":
             # bit-exact MT19937 on the GPU (jump-ahead substreams); the host
             # draw below is the fallback for a rejected draw (odds ~2^-520)
             vb = field.vec_bytes(n)
@@ -265,16 +264,21 @@ class SecretShare(object):
         n = vals.numel()
         t = max(self.threshold, 1)
         vb = field.vec_bytes(n)
+        if out is None:
+            out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
+        elif out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous():
+            raise ValueError(f"make_shares_vec: out must be contiguous uint8 [{shares}, {vb}]")
+        if coeffs is None and t > 1 and n > 0 and shares > 0 and _native.mt_split_device(self.random, vals, out, n, t,
+                                                                                          shares):
+            # fused: the reference's MT19937 draws feed the split in registers (no coefficient block)
+            self.last_draw_rejected = False
+            return out
         if coeffs is None:
             coeffs = self.draw_coeffs_vec(n, dev) if t > 1 else None
         elif t > 1:
             if coeffs.dtype != torch.uint8 or tuple(coeffs.shape) != (t - 1, vb) or coeffs.device != dev:
                 raise ValueError(f"make_shares_vec: coeffs must be uint8 [{t - 1}, {vb}] on {dev}")
             coeffs = coeffs.contiguous()
-        if out is None:
-            out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
-        elif out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous():
-            raise ValueError(f"make_shares_vec: out must be contiguous uint8 [{shares}, {vb}]")
         if shares > 0:
             _native.split_u64(vals, coeffs if t > 1 else None, out, n, t, shares)
         return out

@@ -173,19 +173,37 @@ int dn_mt19937_draw_coeffs(uint32_t* mt_state, int32_t* mt_index, uint64_t n_ele
                            int tm1, void* coeffs);
 
 /*
- * The same draw, bit-exact, with the coefficients generated on the GPU
- * (csrc/mt19937_device.hip): the host computes the MT state at the start of
- * every 17*2^16-word substream by jump-ahead, one wave per substream runs
- * MT19937 from there.  `coeffs` is a DEVICE block of t-1 tiled vectors,
- * `scratch` device memory of dn_mt19937_device_scratch_bytes(n, t-1) bytes.
- * Synchronises `stream`.  On DN_OK the state is advanced exactly as the host
- * draw advances it.  DN_ERR_RETRY (a draw >= p-1 was seen: later words shift,
- * odds ~2^-520 per coefficient) and DN_ERR_UNSUPPORTED (more than 4096
- * substreams) leave the state untouched: draw on the host instead.
+ * The same draw, bit-exact, entirely on the GPU (csrc/mt19937_device.hip):
+ * the MT window at the start of every 17*2^14-word substream by jump-ahead
+ * kernels (at most three levels of independent jumps), then one wave per
+ * substream runs MT19937 from its window.  `coeffs` is a DEVICE block of t-1
+ * tiled vectors, `scratch` device memory of
+ * dn_mt19937_device_scratch_bytes(n, t-1) bytes.  Synchronises `stream`.  On
+ * DN_OK the state is advanced exactly as the host draw advances it.
+ * DN_ERR_RETRY (a draw >= p-1 was seen: later words shift, odds ~2^-520 per
+ * coefficient) and DN_ERR_UNSUPPORTED (more than 262144 substreams) leave the
+ * state untouched: draw on the host instead.
  */
 uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1);
 int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1,
                                   void* coeffs, void* scratch, uint64_t scratch_bytes, void* stream);
+
+/*
+ * make_shares over a vector with the reference's own coefficients, fused:
+ * the device draw above feeding dn_m521_split_u64 in registers — each
+ * substream's wave draws the coefficients of 64 consecutive elements at a
+ * time and writes their n shares, so the coefficient block never reaches
+ * memory (8 + 66 n bytes of HBM per element instead of 8 + 66 n + 4 * 66
+ * (t - 1)).  Same results and final MT state as dn_mt19937_draw_coeffs_device
+ * followed by dn_m521_split_u64.  Scratch: dn_mt19937_device_scratch_bytes(n, t-1).
+ * DN_ERR_UNSUPPORTED: t not in {2, 3, 5} or n too large for forward
+ * differences (use the draw and the split); DN_ERR_RETRY as above (the shares
+ * are then incomplete: redo the draw on the host and split).
+ * Replaces per element: shamir.py:55-66 (make_shares) with :59-61's draws.
+ */
+int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, const int64_t* secrets, void* shares,
+                            uint64_t n_elem, int threshold, int n_shares, void* scratch, uint64_t scratch_bytes,
+                            void* stream);
 
 /*
  * Host.  Advance a CPython MT19937 state by `words` 32-bit outputs (as

@@ -411,6 +411,56 @@ def test_device_mt_draw_equals_host_draw_past_4096_substreams():
     assert a.getstate() == b.getstate()
 
 
+@pytest.mark.parametrize("t,n", [(2, 3), (3, 5), (5, 9), (3, 200)])
+@pytest.mark.parametrize("N", [1, 63, 257, 1000, 8192 + 5, (1 << 20) + 77])
+def test_fused_draw_split_equals_draw_then_split(t, n, N):
+    """make_shares_vec with the reference's coefficients takes the fused
+    device path (dn_mt19937_split_device: the MT19937 draws feed the split in
+    registers): same shares as drawing the block and splitting it, same final
+    random.Random state, from a mid-array start index."""
+    sec = torch.from_numpy(secrets_int64(N + t, N)).to(dev())
+    a, b = shamir.SecretShare(t), shamir.SecretShare(t)
+    a.random.seed(N * 7 + t)
+    a.random.getrandbits(32 * (N % 600))
+    b.random.setstate(a.random.getstate())
+    out = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
+    assert _native.mt_split_device(a.random, sec, out, N, t, n)
+    co = b.draw_coeffs_vec(N, dev())
+    want = torch.empty_like(out)
+    _native.split_u64(sec, co, want, N, t, n)
+    assert np.array_equal(block_limbs(out, N), block_limbs(want, N))
+    assert a.random.getstate() == b.random.getstate()
+
+
+def test_fused_draw_split_declines_and_falls_back():
+    """t outside {2, 3, 5} (and n beyond forward differences) is declined with
+    the state untouched; make_shares_vec then draws and splits, and a forced
+    rejected draw (tuning build) takes the host draw: same shares either way."""
+    N = 3000
+    sec = torch.from_numpy(secrets_int64(11, N)).to(dev())
+    for t, n in ((4, 6), (3, 40000)):
+        r = shamir.SecretShare(t)
+        r.random.seed(5)
+        st = r.random.getstate()
+        out = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
+        assert not _native.mt_split_device(r.random, sec, out, N, t, n)
+        assert r.random.getstate() == st
+    ref = shamir.SecretShare(3)
+    ref.random.seed(9)
+    want = ref.make_shares_vec(sec, 5)
+    with _native.library(_native.TUNING_LIB):
+        import os
+        os.environ["DN_MT_FORCE_RETRY"] = "1"
+        try:
+            ss = shamir.SecretShare(3)
+            ss.random.seed(9)
+            got = ss.make_shares_vec(sec, 5)
+        finally:
+            del os.environ["DN_MT_FORCE_RETRY"]
+    assert np.array_equal(block_limbs(got, N), block_limbs(want, N))  # the valid elements (tile padding unspecified)
+    assert ss.random.getstate() == ref.random.getstate()
+
+
 def test_draw_coeffs_vec_device_path_matches_reference_fixture():
     """draw_coeffs_vec (device MT by default) reproduces the coefficients the
     reference consumed for F1 (tests/golden), and the split from them matches."""
