@@ -519,6 +519,90 @@ def rows_bench(dev, log2n: int) -> dict:
     return rows
 
 
+def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
+    """make_shares_vec(values, 5) with the reference's coefficients (t = 3):
+    MT19937 draws on the GPU (jump-ahead substreams) fused with the split
+    (dn_mt19937_split_device), vs the coefficient block drawn then split.
+    Wall time per call (the call synchronises: it returns CPython's final MT
+    state).  Bytes: 8 + 5 x 66 per element fused (no coefficient block), vs
+    2 x 66 written + 470 for draw then split."""
+    import random
+
+    from delta_node.crypto import shamir
+    from delta_node.crypto.shamir import _native, field
+
+    n = 1 << log2n
+    sec = torch.from_numpy(secrets_int64(5, n)).to(dev)
+    out = torch.empty((5, field.vec_bytes(n)), dtype=torch.uint8, device=dev)
+    fused, unfused = [], []
+    ok = True
+    for r in range(reps + 1):
+        a, b = shamir.SecretShare(3), shamir.SecretShare(3)
+        a.random.seed(77 + r)
+        b.random.seed(77 + r)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        got = a.make_shares_vec(sec, 5, out=out)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        co = b.draw_coeffs_vec(n, dev)
+        want = torch.empty_like(out)
+        _native.split_u64(sec, co, want, n, 3, 5)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        if r:  # the first round warms up
+            fused.append(t1 - t0)
+            unfused.append(t2 - t1)
+        ok = ok and bool(torch.equal(got, want)) and a.random.getstate() == b.random.getstate()
+        del co, want
+    fm, um = min(fused), min(unfused)
+    words = 17 * 2 * n
+    return {"workload": f"make_shares_vec(2^{log2n} int64, 5) on SecretShare(3), coefficients = the reference's "
+                        "MT19937 draws (shamir.py:59-61), bit-exact", "unit": "elements/s",
+            "fused_ms": fm * 1e3, "fused_elems_per_s": n / fm, "draw_then_split_ms": um * 1e3,
+            "draw_then_split_elems_per_s": n / um, "mt_words_per_s_fused": words / fm,
+            "roofline_fused": roof("hbm", n * (8 + 5 * 66) / fm / 1e9,
+                                   "8 B secret + 5 x 66 B shares per element (wall time of the whole call)"),
+            "equal_draw_then_split_and_state": ok}
+
+
+def byte_api_row(budget_s: float = 2.0) -> dict:
+    """The call sites the reference actually has (runner/horizontal/agg.py:142-153,
+    coord/horizontal/agg.py:296,330,362): make_shares of one 32-byte secret into
+    n = 5 / 9 shares and resolve_shares from t of them, per call, beside the
+    reference algorithm restated in pure Python on 1 core."""
+    import os as _os
+
+    from delta_node.crypto import shamir
+    from oracle import py_shamir
+
+    def per_call(fn, budget):
+        fn()
+        k, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            k += 1
+            dt = time.perf_counter() - t0
+            if dt > budget or k >= 20000:
+                return dt / k * 1e6
+
+    out = {"unit": "us per call"}
+    secret = _os.urandom(32)
+    for t, n in ((3, 5), (5, 9)):
+        ss = shamir.SecretShare(t)
+        ref = py_shamir.RefSecretShare(t, seed=1)
+        sh = ss.make_shares(secret, n)
+        rsh = ref.make_shares(secret, n)
+        ok = ss.resolve_shares(sh[:t]) == ref.resolve_shares(rsh[:t]) == secret.lstrip(b"\0")
+        out[f"t{t}n{n}"] = {
+            "make_shares_us": per_call(lambda: ss.make_shares(secret, n), budget_s / 8),
+            "resolve_shares_us": per_call(lambda: ss.resolve_shares(sh[:t]), budget_s / 8),
+            "cpu_reference_make_shares_us": per_call(lambda: ref.make_shares(secret, n), budget_s / 8),
+            "cpu_reference_resolve_shares_us": per_call(lambda: ref.resolve_shares(rsh[:t]), budget_s / 8),
+            "roundtrip_ok": bool(ok)}
+    return out
+
+
 def load_traffic(path: str):
     try:
         with open(path) as f:
@@ -747,6 +831,8 @@ def main():
         line["config4"] = config4_bench(dev, world, rank, args.config4_log2n)
     if args.rows and world == 1:
         line["rows"] = rows_bench(dev, args.log2n)
+        line["rows"]["draw_split"] = draw_split_row(dev, args.log2n)
+        line["rows"]["byte_api"] = byte_api_row()
     if args.config5 and world == 1:
         line["config5"] = config5_bench(args.log2n)
     if rank == 0 and world == 1 and args.cpu_budget > 0:

@@ -27,6 +27,8 @@ DN_ERR_HIP = -5
 DN_ERR_UNSUPPORTED = -6
 DN_ERR_EMPTY = -7
 DN_ERR_RETRY = -8
+DN_ERR_ZERODIV = -9
+DN_ERR_ASSERT = -10
 
 MAX_RESOLVE = 16
 MAX_THRESHOLD = 64
@@ -41,7 +43,7 @@ EXPORTS = (
     "dn_m521_reconstruct", "dn_mt19937_draw_coeffs", "dn_last_error", "dn_version",
     "dn_m521_split_prng", "dn_m521_prng_coeffs",
     "dn_mt19937_device_scratch_bytes", "dn_mt19937_draw_coeffs_device", "dn_mt19937_skip",
-    "dn_mt19937_split_device",
+    "dn_mt19937_split_device", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
 )
 
 
@@ -138,6 +140,12 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_mt19937_split_device.restype = i32
     L.dn_mt19937_split_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), vp, vp, u64,
                                           i32, i32, vp, u64, vp]
+    L.dn_shamir_make_shares_host.restype = i32
+    L.dn_shamir_make_shares_host.argtypes = [ctypes.c_char_p, u64, ctypes.c_char_p, ctypes.c_uint32, i32,
+                                             ctypes.c_char_p, ctypes.c_uint32, u64, vp, u64, vp]
+    L.dn_shamir_resolve_shares_host.restype = i32
+    L.dn_shamir_resolve_shares_host.argtypes = [ctypes.c_char_p, vp, i32, i32, ctypes.c_char_p, ctypes.c_uint32, vp,
+                                                u64, ctypes.POINTER(ctypes.c_uint64)]
     L.dn_mt19937_skip.restype = i32
     L.dn_mt19937_skip.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64]
     L.dn_last_error.restype = ctypes.c_char_p
@@ -162,6 +170,10 @@ def check(rc: int) -> None:
         raise TypeError(msg)
     if rc == DN_ERR_UNSUPPORTED:
         raise NotImplementedError(msg)
+    if rc == DN_ERR_ZERODIV:
+        raise ZeroDivisionError
+    if rc == DN_ERR_ASSERT:
+        raise AssertionError
     raise RuntimeError(f"dn_shamir error {rc}: {msg}")
 
 
@@ -327,6 +339,56 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
     check(rc)
     rng.setstate((version, tuple(state) + (index.value,), gauss))
     return True
+
+
+# ------------------------------------------------------------------ host (byte API)
+M521 = (1 << 521) - 1
+
+
+def _prime_arg(prime: int):
+    if prime == M521:
+        return None, 0, 66
+    pb = prime.to_bytes(max(1, (prime.bit_length() + 7) // 8), "big")
+    return pb, len(pb), len(pb)
+
+
+def host_make_shares(value: bytes, coeffs: Sequence[int], prime: int, threshold: int, n: int) -> List[bytes]:
+    """The reference's make_shares arithmetic for one secret on the host
+    (dn_shamir_make_shares_host, csrc/host_shamir.cpp): `value` is coefficient
+    0 as the caller's bytes, `coeffs` the t-1 drawn coefficients; returns the
+    n share records ([len(x)][x][y], shamir.py:28-33)."""
+    pb, plen, w = _prime_arg(prime)
+    cb = b"".join([c.to_bytes(w, "big") for c in coeffs])
+    cap = n * (9 + w)
+    out = ctypes.create_string_buffer(cap)
+    offs = (ctypes.c_uint64 * (n + 1))()
+    rc = (_lib or lib()).dn_shamir_make_shares_host(value, len(value), cb, w, threshold, pb, plen, n, out, cap, offs)
+    if rc:
+        check(rc)
+    raw = ctypes.string_at(out, offs[n])
+    o = offs[:]
+    return [raw[o[i]:o[i + 1]] for i in range(n)]
+
+
+def host_resolve_shares(shares: Sequence[bytes], threshold: int, prime: int) -> bytes:
+    """The reference's resolve_shares arithmetic on the host
+    (dn_shamir_resolve_shares_host): parse, checks (same messages), Lagrange
+    at 0 over all k shares, minimal big-endian bytes."""
+    pb, plen, w = _prime_arg(prime)
+    k = len(shares)
+    offs = (ctypes.c_uint64 * (k + 1))()
+    o = 0
+    for i, s in enumerate(shares):
+        offs[i] = o
+        o += len(s)
+    offs[k] = o
+    out = ctypes.create_string_buffer(w + 8)
+    n = ctypes.c_uint64(0)
+    rc = (_lib or lib()).dn_shamir_resolve_shares_host(b"".join(shares), offs, k, threshold, pb, plen, out, w + 8,
+                                                       ctypes.byref(n))
+    if rc:
+        check(rc)
+    return ctypes.string_at(out, n.value)
 
 
 def version() -> str:

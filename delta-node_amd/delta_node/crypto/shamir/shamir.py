@@ -13,9 +13,10 @@ reference (shamir.py)          here
 ``_bytes_to_share`` :36-45     same codec (host, per share)
 ``SecretShare.__init__`` :49   same attributes: threshold, prime, random
 ``make_shares`` :55-66         coefficients from ``self.random`` exactly as
-                               the reference draws them; evaluation on GPU
-``resolve_shares`` :68-90      same checks/messages; Lagrange weights on the
-                               host (once per call), interpolation on GPU
+                               the reference draws them; evaluation in the
+                               library's host path (one secret per call)
+``resolve_shares`` :68-90      same checks/messages/exceptions, library host
+                               path (any prime)
 =============================  =============================================
 
 Vector extension (the hot path, new): ``make_shares_vec`` splits a whole
@@ -23,9 +24,11 @@ int64 tensor, element e behaving exactly like
 ``make_shares(v_e.to_bytes(8, "big", signed=True), n)`` called in order on the
 same instance; ``resolve_shares_vec`` interpolates whole share vectors.
 
-There is no CPU fallback: without the native library or a HIP device every
-call raises.  Only the default prime (the Mersenne prime M521) is supported;
-``SecretShare(t, prime=q)`` with another q raises NotImplementedError.
+There is no CPU fallback: without the native library every call raises, and
+without a HIP device every vector call raises.  The byte API (one secret per
+call, as the reference's callers use it) runs in the library's native host
+path (csrc/host_shamir.cpp) for any prime, like the reference's
+``SecretShare(t, prime=q)``; the vector API is GF(2^521 - 1) on the GPU.
 """
 from __future__ import annotations
 
@@ -150,47 +153,40 @@ class SecretShare(object):
     """Threshold-`threshold` Shamir scheme over GF(PRIME) (shamir.py:48-90)."""
 
     def __init__(self, threshold: int, *, prime: int = PRIME):
-        if prime != PRIME:
-            raise NotImplementedError("the MI355X Shamir path supports only the default prime 2^521 - 1")
         self.threshold = threshold
         self.prime = prime
         self.random = random.Random()
         self.last_draw_rejected = False
 
+    def _require_m521(self):
+        if self.prime != PRIME:
+            raise NotImplementedError("the vector (GPU) path is GF(2^521 - 1) only; the byte API takes any prime")
+
     # ---- reference byte API -------------------------------------------
     def make_shares(self, value: bytes, shares: int) -> List[bytes]:
-        """Split `value` into `shares` byte shares (shamir.py:55-66)."""
+        """Split `value` into `shares` byte shares (shamir.py:55-66).
+
+        One secret per call — the reference's callers' pattern — so the field
+        arithmetic runs in the library's host path (dn_shamir_make_shares_host:
+        a GPU launch and two copies would cost ~20x the reference's latency);
+        the coefficients are drawn from `self.random` exactly as the reference
+        draws them."""
         if self.threshold > shares:
             raise ValueError("threshold should be little equal than shares")
-        coeffs = [serialize.bytes_to_int(value)] + [
-            self.random.randint(1, self.prime - 1) for _ in range(self.threshold - 1)
-        ]
+        serialize.bytes_to_int(value)  # the reference's conversion (and its errors)
+        coeffs = [self.random.randint(1, self.prime - 1) for _ in range(self.threshold - 1)]
         if shares <= 0:
             return []
-        if shares > _native.MAX_SHARES or len(coeffs) > _native.MAX_THRESHOLD:
-            raise NotImplementedError("make_shares: at most 65535 shares and threshold 64 on the device path")
-        ys = _eval_many(coeffs, shares)
-        return [_share_to_bytes((x, y)) for x, y in zip(range(1, shares + 1), ys)]
+        return _native.host_make_shares(bytes(value), coeffs, self.prime, self.threshold, shares)
 
     def resolve_shares(self, shares: List[bytes]) -> bytes:
         """Recover the secret from byte shares (shamir.py:68-90): the
-        Lagrange interpolant of ALL given shares at 0, minimal big-endian."""
-        import torch
-
-        share_tups = [_bytes_to_share(share) for share in shares]
-        xs, ys = zip(*share_tups)
-        k = len(xs)
-        if k < self.threshold:
-            raise ValueError("need at least {} shares".format(self.threshold))
-        if k != len(set(xs)):
-            raise ValueError("shares must be distinct")
-        if k == 1:  # the reference's reduce() over an empty product list
-            raise TypeError("reduce() of empty iterable with no initial value")
-        dev = _device()
-        vecs = list(_to_device_vecs([y % PRIME for y in ys], dev).unbind(0))
-        out = torch.empty(field.vec_bytes(1), dtype=torch.uint8, device=dev)
-        _resolve_vectors(vecs, xs, 1, self.threshold, out_fe=out)
-        return serialize.int_to_bytes(field.vec_to_ints(out.cpu().numpy(), 1)[0])
+        Lagrange interpolant of ALL given shares at 0, minimal big-endian, with
+        the reference's checks and messages (dn_shamir_resolve_shares_host)."""
+        shares = [bytes(s) for s in shares]
+        if not shares:  # zip(*[]) unpacked into xs, ys
+            raise ValueError("not enough values to unpack (expected 2, got 0)")
+        return _native.host_resolve_shares(shares, self.threshold, self.prime)
 
     # ---- vector extension (the hot path) -------------------------------
     def draw_coeffs_vec(self, n: int, device=None, *, elem_offset: int = 0, n_total: Optional[int] = None):
@@ -205,6 +201,7 @@ class SecretShare(object):
         unless a 521-bit draw is rejected (odds ~2^-520 each) in the skipped
         range; `self.last_draw_rejected` reports one in this shard's range, and
         `dist.draw_coeffs_sharded` combines the flags over ranks."""
+        self._require_m521()
         import torch
 
         dev = device if device is not None else _device()
@@ -250,6 +247,7 @@ class SecretShare(object):
         Returns uint8 device tensor [shares, vec_bytes(N)]: row x-1 holds share x
         of every element (tiled M521 layout, canonical residues).
         """
+        self._require_m521()
         import torch
 
         if self.threshold > shares:
@@ -294,6 +292,7 @@ class SecretShare(object):
         unsharded result.  key: 32 bytes (default: fresh from `secrets`);
         rounds: 20 (default), 12 or 8.  Returns (shares block, key).
         """
+        self._require_m521()
         import secrets as _secrets
 
         import torch
@@ -333,6 +332,7 @@ class SecretShare(object):
         return_overflow  also return a uint32 device counter of elements >= 2^64
         Same checks as `resolve_shares` (too few, duplicates, k == 1).
         """
+        self._require_m521()
         import torch
 
         vecs = list(shares.unbind(0)) if isinstance(shares, torch.Tensor) and shares.dim() == 2 else list(shares)

@@ -60,7 +60,9 @@ enum {
   DN_ERR_HIP = -5,         /* HIP runtime error (launch failure)                   */
   DN_ERR_UNSUPPORTED = -6, /* outside the limits above                             */
   DN_ERR_EMPTY = -7,       /* shamir.py:78-83  k == 1: reduce() of empty iterable  */
-  DN_ERR_RETRY = -8        /* device MT draw hit a rejected draw: redo on the host */
+  DN_ERR_RETRY = -8,       /* device MT draw hit a rejected draw: redo on the host */
+  DN_ERR_ZERODIV = -9,     /* op.py:17-18      inverse_mod(0, p): ZeroDivisionError */
+  DN_ERR_ASSERT = -10      /* op.py:22-23      gcd(k, p) != 1: AssertionError      */
 };
 
 /* Bytes of one tiled field-element vector of n elements (66 * round_up(n, 256)). */
@@ -204,6 +206,33 @@ int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_
 int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, const int64_t* secrets, void* shares,
                             uint64_t n_elem, int threshold, int n_shares, void* scratch, uint64_t scratch_bytes,
                             void* stream);
+
+/*
+ * Host.  The byte API for one secret per call (csrc/host_shamir.cpp), the way
+ * the reference's callers use it (runner/horizontal/agg.py:142-153,
+ * coord/horizontal/agg.py:296,330,362), in any prime field (shamir.py:49-51).
+ *   prime_be / prime_len  big-endian p; NULL or 2^521 - 1 takes the fixed
+ *                         9 x 64-bit Mersenne path
+ *
+ * make_shares (shamir.py:55-66, _eval_at :19-25, _share_to_bytes :28-33):
+ *   value / value_len     coefficient 0 as the caller's bytes (bytes_to_int)
+ *   coeffs_be             t-1 coefficients, coeff_bytes big-endian bytes each
+ *   out, out_cap          records [len(x)][x][y] back to back, capacity
+ *                         >= n_shares * (9 + len(p)); offsets[n_shares + 1]
+ * DN_ERR_THRESHOLD if t > n_shares.
+ *
+ * resolve_shares (shamir.py:68-90, _bytes_to_share :36-45, op.py:4-29):
+ *   shares, offsets       k records back to back, offsets[k + 1]
+ *   out, out_cap, out_len the secret, minimal big-endian
+ * DN_ERR_TOO_FEW / DN_ERR_DISTINCT / DN_ERR_EMPTY as dn_m521_lagrange;
+ * DN_ERR_ZERODIV / DN_ERR_ASSERT where op.inverse_mod raises.
+ */
+int dn_shamir_make_shares_host(const uint8_t* value, uint64_t value_len, const uint8_t* coeffs_be,
+                               uint32_t coeff_bytes, int threshold, const uint8_t* prime_be, uint32_t prime_len,
+                               uint64_t n_shares, uint8_t* out, uint64_t out_cap, uint64_t* offsets);
+int dn_shamir_resolve_shares_host(const uint8_t* shares, const uint64_t* offsets, int k, int threshold,
+                                  const uint8_t* prime_be, uint32_t prime_len, uint8_t* out, uint64_t out_cap,
+                                  uint64_t* out_len);
 
 /*
  * Host.  Advance a CPython MT19937 state by `words` 32-bit outputs (as

@@ -1,0 +1,20 @@
+#!/usr/bin/env python3
+"""Run selected bench.py rows alone (one JSON line): ROWS=byte_api,draw_split python scripts/rows_probe.py"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+import torch  # noqa: E402
+
+dev = torch.device("cuda", 0)
+out = {}
+for r in os.environ.get("ROWS", "byte_api,draw_split").split(","):
+    if r == "byte_api":
+        out[r] = bench.byte_api_row()
+    elif r == "draw_split":
+        out[r] = bench.draw_split_row(dev, int(os.environ.get("LOG2N", "24")))
+print(json.dumps(out))

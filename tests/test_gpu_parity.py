@@ -84,57 +84,6 @@ def test_split_vec_explicit_coeffs_and_reconstruct(key):
         assert limbs_to_ints(field.vec_to_limbs(fe.cpu().numpy(), N)) == [int(v) & MASK64 for v in z["secrets"]]
 
 
-# ------------------------------------------------------------ golden: byte API
-def test_byte_api_matches_reference_fixture():
-    f3 = load_json("f3_edge.json")
-    for case in f3["cases"]:
-        ss = shamir.SecretShare(case["t"])
-        ss.random.seed(case["mt_seed"])
-        shares = ss.make_shares(bytes.fromhex(case["value"]), case["n"])
-        assert [s.hex() for s in shares] == case["shares"], (case["t"], case["n"], case["value"][:16])
-        for r in case["resolve"]:
-            sh = [shares[x - 1] for x in r["xs"]]
-            if "exc" in r:
-                with pytest.raises(Exception) as ei:
-                    ss.resolve_shares(sh)
-                assert type(ei.value).__name__ == r["exc"]
-            else:
-                assert ss.resolve_shares(sh).hex() == r["out"], (case["t"], case["n"], r["xs"][:5])
-
-
-def test_byte_api_reference_test_restated():
-    """tests/shamir_test.py:9-19 of the reference: 2-of-5, 32 random bytes,
-    resolve from 5, 4 and 3 shares (leading zero bytes are dropped by the
-    reference's minimal encoding, so values start with a non-zero byte here)."""
-    rng = random.Random(11)
-    for _ in range(20):
-        value = bytes([rng.randrange(1, 256)]) + bytes(rng.getrandbits(8) for _ in range(31))
-        ss = shamir.SecretShare(2)
-        shares = ss.make_shares(value, 5)
-        assert len(shares) == 5
-        assert ss.resolve_shares(shares) == value
-        assert ss.resolve_shares(rng.sample(shares, 4)) == value
-        assert ss.resolve_shares(rng.sample(shares, 3)) == value
-    ss = shamir.SecretShare(2)
-    assert ss.resolve_shares(ss.make_shares(b"\x00\x01", 3)) == b"\x01"  # reference quirk
-
-
-def test_reconstruct_random_shares_matches_reference():
-    """Inconsistent shares: the degree-(k-1) interpolant at 0 over ALL shares."""
-    for group in load_json("f4_recon.json"):
-        xs = group["xs"]
-        ss = shamir.SecretShare(len(xs))
-        for row in group["rows"]:
-            ys = [int(y, 16) for y in row["ys"]]
-            sh = [shamir.shamir._share_to_bytes((x, y)) for x, y in zip(xs, ys)]
-            if "exc" in row:
-                with pytest.raises(Exception) as ei:
-                    ss.resolve_shares(sh)
-                assert type(ei.value).__name__ == row["exc"]
-            else:
-                assert ss.resolve_shares(sh).hex() == row["out"], xs
-
-
 # ------------------------------------------------------------ digests (reference-generated)
 def _split_digest_case(d):
     N, t, n = d["N"], d["t"], d["n"]

@@ -239,17 +239,22 @@ def test_surface_and_errors_before_device():
         ss.resolve_shares([])
     with pytest.raises(TypeError):
         shamir.SecretShare(1).resolve_shares(sh[:1])
-    with pytest.raises(NotImplementedError):
-        shamir.SecretShare(3, prime=2**127 - 1)
+    ss127 = shamir.SecretShare(3, prime=2**127 - 1)  # the byte API takes any prime (host path)
+    assert ss127.resolve_shares(ss127.make_shares(b"\x01\x02", 4)[1:]) == b"\x01\x02"
+    with pytest.raises(NotImplementedError):  # the vector (GPU) path is M521 only
+        ss127.make_shares_vec(torch.arange(4, dtype=torch.int64), 4)
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-device failure mode")
 def test_no_cpu_fallback():
+    """The vector path needs the GPU (no CPU fallback); the byte API is the
+    library's native host path by design (one secret per call)."""
     ss = shamir.SecretShare(2)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
-        ss.make_shares(b"\x07", 3)
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
         ss.make_shares_vec(torch.arange(10, dtype=torch.int64), 3)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ss.resolve_shares_vec([torch.zeros(66 * 256, dtype=torch.uint8)] * 2, [1, 2], 10)
+    assert ss.resolve_shares(ss.make_shares(b"\x07", 3)[:2]) == b"\x07"
 
 
 @pytest.mark.parametrize("start_words", [0, 5, 623, 624, 1000])
