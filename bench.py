@@ -496,6 +496,27 @@ def rows_bench(dev, log2n: int) -> dict:
                "mont_mul_per_s": ((1 << 20) * 10 * 13 * 4 + 8192 * 127 * 2 * 13 * 4) / (bm * 1e-3),
                "oracle_prefix_equal": broots[:1] == bwant}
     del bdev
+    # calc_weight_commitment (mimc7.py:58-60): one sequential chain, host core (dn_mimc7_weight_commitment_host)
+    # beside the same chain on one device lane (dn_mimc7_weight_chain) and the Python restatement
+    wts = drng.standard_normal(1 << 17) * 0.1
+    t0 = time.perf_counter()
+    wc = mimc7.calc_weight_commitment(wts)
+    wh = time.perf_counter() - t0
+    wdev = torch.from_numpy(wts[:4096]).to(dev)
+    mimc7.weight_commitment_device(wdev[:16])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    wd = mimc7.weight_commitment_device(wdev)
+    wdt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    wp = py_mimc7.weight_commitment(wts[:4096])
+    wpt = time.perf_counter() - t0
+    weight_row = {"workload": "calc_weight_commitment of 2^17 float64 weights (52 dependent products each)",
+                  "host_us_per_weight": wh / (1 << 17) * 1e6,
+                  "device_lane_us_per_weight": wdt / 4096 * 1e6,
+                  "cpu_python_us_per_weight": wpt / 4096 * 1e6,
+                  "oracle_equal_4096": wd == wp and mimc7.calc_weight_commitment(wts[:4096]) == wp,
+                  "commitment_prefix": wc.hex()[:16]}
     rows["mimc7_commitment"] = {"workload": "calc_data_commitment, 2^15 rows x 10 cols -> 256 roots",
                                 "ms": mm, "rows_per_s": (1 << 15) / (mm * 1e-3),
                                 "mont_mul_per_s": mulmods / (mm * 1e-3),
@@ -503,7 +524,7 @@ def rows_bench(dev, log2n: int) -> dict:
                                                "128-row Merkle block: latency-bound chains at this size",
                                 "oracle_prefix_equal": roots[:2] == want, "bound": "valu (BN254 Montgomery mul)",
                                 "cpu_python": {"rows_per_s": 256 / cdt, "sample": "256 rows, Python ints 1 thread"},
-                                "at_2e20_rows": big_row}
+                                "at_2e20_rows": big_row, "weight_commitment": weight_row}
     rows["mask_masking"] = {
         "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
         "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),

@@ -23,12 +23,12 @@
 
 #include "dn_internal.hpp"
 #include "dn_mimc7.h"
+#include "mimc7_consts.hpp"
 
 namespace dn {
 namespace mimc {
 
 constexpr int L = 8;
-constexpr int kRounds = 13;
 
 struct Consts {
   uint32_t q[L];
@@ -332,9 +332,8 @@ __global__ void __launch_bounds__(256) hash_kernel(const HashArgs a) {
 
 // ---- host: constants ----
 void make_consts(Consts& k) {
-  static const uint32_t q[L] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
-                                0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
-  std::memcpy(k.q, q, sizeof(q));
+  const uint32_t* q = kQ32;
+  std::memcpy(k.q, q, sizeof(k.q));
   // qinv = -q^{-1} mod 2^32 (Newton)
   uint32_t inv = q[0];
   for (int i = 0; i < 5; ++i) inv *= 2u - q[0] * inv;
@@ -359,35 +358,6 @@ using namespace dn;
 using namespace dn::mimc;
 
 namespace {
-// Round constants: decimal strings of utils/constant.py:14-30 (the circomlib
-// MiMC7 constants), parsed once per call into 8 limbs and Montgomery form.
-const char* kCtsDec[kRounds] = {
-    "0",
-    "20888961410941983456478427210666206549300505294776164667214940546594746570981",
-    "15265126113435022738560151911929040668591755459209400716467504685752745317193",
-    "8334177627492981984476504167502758309043212251641796197711684499645635709656",
-    "1374324219480165500871639364801692115397519265181803854177629327624133579404",
-    "11442588683664344394633565859260176446561886575962616332903193988751292992472",
-    "2558901189096558760448896669327086721003508630712968559048179091037845349145",
-    "11189978595292752354820141775598510151189959177917284797737745690127318076389",
-    "3262966573163560839685415914157855077211340576201936620532175028036746741754",
-    "17029914891543225301403832095880481731551830725367286980611178737703889171730",
-    "4614037031668406927330683909387957156531244689520944789503628527855167665518",
-    "19647356996769918391113967168615123299113119185942498194367262335168397100658",
-    "5040699236106090655289931820723926657076483236860546282406111821875672148900"};
-
-void dec_to_limbs(const char* s, uint32_t out[L]) {
-  for (int i = 0; i < L; ++i) out[i] = 0;
-  for (; *s; ++s) {  // out = out * 10 + digit
-    uint64_t c = static_cast<uint64_t>(*s - '0');
-    for (int i = 0; i < L; ++i) {
-      const uint64_t t = static_cast<uint64_t>(out[i]) * 10u + c;
-      out[i] = static_cast<uint32_t>(t);
-      c = t >> 32;
-    }
-  }
-}
-
 void consts(Consts& k) {
   std::memset(&k, 0, sizeof(k));
   make_consts(k);
@@ -398,11 +368,6 @@ void consts(Consts& k) {
   }
 }
 
-double pow10d(int p) {
-  double s = 1.0;
-  for (int i = 0; i < p; ++i) s *= 10.0;
-  return s;
-}
 }  // namespace
 
 extern "C" int dn_mimc7_data_rows(const double* data, uint64_t rows, int cols, uint32_t* row_hashes,

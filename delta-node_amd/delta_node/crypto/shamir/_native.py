@@ -29,6 +29,7 @@ DN_ERR_EMPTY = -7
 DN_ERR_RETRY = -8
 DN_ERR_ZERODIV = -9
 DN_ERR_ASSERT = -10
+DN_ERR_OVERFLOW = -11
 
 MAX_RESOLVE = 16
 MAX_THRESHOLD = 64
@@ -174,6 +175,8 @@ def check(rc: int) -> None:
         raise ZeroDivisionError
     if rc == DN_ERR_ASSERT:
         raise AssertionError
+    if rc == DN_ERR_OVERFLOW:
+        raise OverflowError(msg)
     raise RuntimeError(f"dn_shamir error {rc}: {msg}")
 
 

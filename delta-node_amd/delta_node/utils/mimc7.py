@@ -4,8 +4,12 @@ Reference: delta_node/utils/mimc7.py:18-92, `__all__ = ["calc_weight_commitment"
 "calc_data_commitment"]` (gmpy2 arithmetic over the BN254 scalar field,
 utils/constant.py).  Same names, inputs and outputs; the row hashes and the
 Merkle trees of calc_data_commitment run one lane per row / one workgroup per
-128-row block (dn_mimc7_data_rows, dn_mimc7_merkle_blocks); the weight
-commitment is one sequential chain (dn_mimc7_weight_chain, one lane).
+128-row block on the GPU (dn_mimc7_data_rows, dn_mimc7_merkle_blocks); the
+weight commitment is one strictly sequential chain of dependent field products
+and runs natively on the calling host core (dn_mimc7_weight_commitment_host,
+csrc/host_mimc7.cpp — see its header for the measured reason), exact for every
+finite weight.  dn_mimc7_weight_chain is the same chain on one device lane, for
+device-resident weights (weight_commitment_device).
 """
 from __future__ import annotations
 
@@ -21,7 +25,8 @@ __all__ = ["calc_weight_commitment", "calc_data_commitment"]
 
 Q = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 DATA_BLOCK = 128
-EXPORTS = ("dn_mimc7_data_rows", "dn_mimc7_merkle_blocks", "dn_mimc7_weight_chain", "dn_mimc7_hash")
+EXPORTS = ("dn_mimc7_data_rows", "dn_mimc7_merkle_blocks", "dn_mimc7_weight_chain", "dn_mimc7_hash",
+           "dn_mimc7_weight_commitment_host", "dn_mimc7_params")
 def _lib():
     L = _native.lib()
     if not getattr(L, "_dn_mimc7_bound", False):  # argtypes, once per loaded library
@@ -34,6 +39,8 @@ def _lib():
         L.dn_mimc7_weight_chain.argtypes = [vp, u64, i32, vp, vp, vp]
         L.dn_mimc7_hash.restype = i32
         L.dn_mimc7_hash.argtypes = [vp, vp, u64, vp, vp]
+        L.dn_mimc7_weight_commitment_host.restype = i32
+        L.dn_mimc7_weight_commitment_host.argtypes = [vp, u64, i32, vp]
         L._dn_mimc7_bound = True
     return L
 
@@ -96,11 +103,34 @@ def calc_data_commitment(data: Iterable[Iterable[float]]) -> List[bytes]:
 
 
 def calc_weight_commitment(weight: Iterable[float]) -> bytes:
-    """mimc7.py:58-60."""
+    """mimc7.py:58-60: mimc7_hash_arr([_float2mpz(w, 8) for w in weight], 2), minimal big-endian bytes.
+
+    Weights are converted to float64 first (numpy 1.22 value-based casting makes
+    the reference's float32 * 10**8 a float64 product too).  A torch tensor is
+    read back to the host.  NaN raises ValueError, +-inf OverflowError, as
+    int() does in the reference.
+    """
+    if hasattr(weight, "detach"):  # torch tensor
+        weight = weight.detach().cpu().numpy()
+    w = np.ascontiguousarray(np.asarray(weight if isinstance(weight, np.ndarray) else list(weight),
+                                        dtype=np.float64).reshape(-1))
+    out = (ctypes.c_uint32 * 8)()
+    _native.check(_lib().dn_mimc7_weight_commitment_host(w.ctypes.data if w.size else None, w.size, 8,
+                                                         ctypes.addressof(out)))
+    return serialize.int_to_bytes(int.from_bytes(bytes(out), "little"))
+
+
+def weight_commitment_device(weight) -> bytes:
+    """The same chain on one device lane (dn_mimc7_weight_chain) for a device float64 tensor.
+
+    Latency-bound (one dependent product at a time on one lane): slower than
+    calc_weight_commitment's host chain; |w * 10^8| >= 2^253 raises
+    NotImplementedError.
+    """
     import torch
 
     dev = _native.require_device()
-    w = torch.as_tensor(np.asarray(list(weight), dtype=np.float64)).to(dev).contiguous()
+    w = torch.as_tensor(weight).to(dev).to(torch.float64).contiguous().reshape(-1)
     out = torch.empty(8, dtype=torch.int32, device=dev)
     bad = torch.zeros(1, dtype=torch.int32, device=dev)
     _native.check(_lib().dn_mimc7_weight_chain(w.data_ptr(), w.numel(), 8, out.data_ptr(), bad.data_ptr(),

@@ -42,6 +42,20 @@ int dn_mimc7_merkle_blocks(const uint32_t* leaves, uint64_t blocks, uint32_t* ro
 int dn_mimc7_weight_chain(const double* w, uint64_t n, int precision, uint32_t* out, uint32_t* bad_count,
                           void* stream);
 
+/* calc_weight_commitment (mimc7.py:58-60) on the calling host core: w is
+ * HOST float64 [n]; out: host uint32[8] = the commitment as a plain field
+ * element.  The chain is strictly sequential (52 dependent field products
+ * per weight), so it runs where a dependent product is cheapest; exact
+ * _float2mpz for every finite double; NaN -> DN_ERR_ARG (ValueError),
+ * +-inf -> DN_ERR_OVERFLOW (OverflowError), as int() raises in mimc7.py:41.
+ * This is the path calc_weight_commitment takes; dn_mimc7_weight_chain is the
+ * single-lane device form of the same chain (kept for device-resident data). */
+int dn_mimc7_weight_commitment_host(const double* w, uint64_t n, int precision, uint32_t* out);
+
+/* Field parameters of utils/constant.py:6-30 as plain 8-limb integers:
+ * q[8] and cts[13][8] (host memory). */
+int dn_mimc7_params(uint32_t* q, uint32_t* cts);
+
 /* Batched mimc7_hash(x_i, key_i) for plain field elements (< q): out is
  * device uint32 [n][9] holding the unreduced r + key (< 2q), as mimc7.py:26. */
 int dn_mimc7_hash(const uint32_t* xs, const uint32_t* keys, uint64_t n, uint32_t* out, void* stream);

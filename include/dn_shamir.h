@@ -62,7 +62,8 @@ enum {
   DN_ERR_EMPTY = -7,       /* shamir.py:78-83  k == 1: reduce() of empty iterable  */
   DN_ERR_RETRY = -8,       /* device MT draw hit a rejected draw: redo on the host */
   DN_ERR_ZERODIV = -9,     /* op.py:17-18      inverse_mod(0, p): ZeroDivisionError */
-  DN_ERR_ASSERT = -10      /* op.py:22-23      gcd(k, p) != 1: AssertionError      */
+  DN_ERR_ASSERT = -10,     /* op.py:22-23      gcd(k, p) != 1: AssertionError      */
+  DN_ERR_OVERFLOW = -11    /* mimc7.py:41      int(inf): OverflowError              */
 };
 
 /* Bytes of one tiled field-element vector of n elements (66 * round_up(n, 256)). */
