@@ -130,7 +130,9 @@ def weight_commitment_device(weight) -> bytes:
     import torch
 
     dev = _native.require_device()
-    w = torch.as_tensor(weight).to(dev).to(torch.float64).contiguous().reshape(-1)
+    if not isinstance(weight, torch.Tensor):  # lists would otherwise become float32 tensors
+        weight = torch.from_numpy(np.asarray(weight, dtype=np.float64).reshape(-1).copy())
+    w = weight.to(dev).to(torch.float64).contiguous().reshape(-1)
     out = torch.empty(8, dtype=torch.int32, device=dev)
     bad = torch.zeros(1, dtype=torch.int32, device=dev)
     _native.check(_lib().dn_mimc7_weight_chain(w.data_ptr(), w.numel(), 8, out.data_ptr(), bad.data_ptr(),
