@@ -84,7 +84,43 @@ def cpu_baseline(t: int, n: int, xs, budget_s: float, procs: int = 16) -> dict:
                           "sample": f"{sum(d for d, _ in res)} elements over {procs} processes, {half:.1f} s each"}
     except Exception as e:  # a box without spare cores: report the 1-core figure only
         out["sharded"] = {"error": repr(e)}
+    out["c_port"] = c_port_baseline(t, n, xs, half, procs)
     return out
+
+
+def c_port_baseline(t: int, n: int, xs, budget_s: float, threads: int) -> dict:
+    """SURVEY §8(d)(iii), the fair-CPU comparison: the same per-element work
+    in C (oracle/m521_oracle.c: CPython MT19937 draw of the coefficients, the
+    reference's Horner with a literal % p, its Lagrange sequence — 9x64-bit
+    limbs) on 1 thread and on `threads` threads (ctypes drops the GIL), chunks
+    of 2^14 elements, time-bounded."""
+    import concurrent.futures as cf
+
+    from oracle import c_oracle
+
+    chunk = 1 << 14
+    rng = np.random.default_rng(3)
+    sec = rng.integers(-2 ** 62, 2 ** 62, chunk, dtype=np.int64)
+
+    def work(seed: int, budget: float):
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            co = c_oracle.draw_coeffs(seed + done, chunk, t - 1)
+            sh = c_oracle.split(sec, co, t, n)
+            c_oracle.reconstruct(sh[[x - 1 for x in xs]], xs)
+            done += chunk
+        return done, time.perf_counter() - t0
+
+    d1, s1 = work(11, budget_s / 4)
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(lambda i: work(1000 * i, budget_s / 2), range(threads)))
+    wall = time.perf_counter() - t0
+    total = sum(d for d, _ in res)
+    return {"value": total / wall, "unit": "elements/s", "cores": threads, "kind": "port",
+            "one_thread": d1 / s1,
+            "sample": f"{total} elements over {threads} threads (chunks of {chunk}: MT19937 draw + split t={t} "
+                      f"n={n} + reconstruct xs={list(xs)}), C restatement, {wall:.1f} s wall"}
 
 
 def measure_ceiling(dev, sec, coeffs, shares, N: int, t: int, n: int, reps: int = 5) -> dict:
@@ -322,10 +358,10 @@ def envelope_row(recs, reps: int, s, e) -> dict:
     return row
 
 
-def rows_bench(dev, log2n: int) -> dict:
-    """SURVEY §8(f) rows measured beside the headline (device-resident inputs):
-    mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
-    pairwise masks (runner/horizontal/agg.py:284-318 with |u2| = 10)."""
+def mask_row(dev, log2n: int) -> dict:
+    """mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
+    pairwise masks (runner/horizontal/agg.py:284-318 with |u2| = 10), one
+    dn_bounded_i64_accumulate launch over 10 generators."""
     import os as _os
 
     from delta_node.utils import masked_sum
@@ -360,7 +396,28 @@ def rows_bench(dev, log2n: int) -> dict:
     for sd, sg in terms:
         acc = acc + sg * pm.make_mask_numpy(sd, vs.shape)
     cpu_dt = time.perf_counter() - t0
+    return {
+        "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
+        "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
+        "roofline": roof("hbm", 16 * n / (ms * 1e-3) / 1e9, "8 B float64 in + 8 B int64 out per element"),
+        "bound": "valu (PCG64 128-bit LCG step + XSL-RR + 64x64 Lemire multiply per draw)",
+        # 49.6 VALU instructions per draw: the ISA of bounded_acc_kernel's
+        # 16-draw loop body (793 VALU), 14 of them half-rate 32x32->64
+        # multiplies (tools/valu_rates.hip: mad_u64 at ~0.57x the add rate)
+        "roofline_valu": roof("valu", 10 * n / (ms * 1e-3) * 49.6 / 1e9,
+                              "49.6 VALU instructions per draw (ISA count), 10 draws per element"),
+        "numpy_prefix_equal": ok,
+        "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}
+
+
+def rows_bench(dev, log2n: int) -> dict:
+    """SURVEY §8(f) rows measured beside the headline (device-resident inputs):
+    mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
+    pairwise masks (runner/horizontal/agg.py:284-318 with |u2| = 10)."""
+    n = 1 << log2n
     rows = {}
+    reps = 5
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     # share wire codec: encode / decode share x=3 of a 2^log2n vector (reference _share_to_bytes records)
     from delta_node.crypto.shamir import codec, field as _field
 
@@ -525,18 +582,7 @@ def rows_bench(dev, log2n: int) -> dict:
                                 "oracle_prefix_equal": roots[:2] == want, "bound": "valu (BN254 Montgomery mul)",
                                 "cpu_python": {"rows_per_s": 256 / cdt, "sample": "256 rows, Python ints 1 thread"},
                                 "at_2e20_rows": big_row, "weight_commitment": weight_row}
-    rows["mask_masking"] = {
-        "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
-        "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
-        "roofline": roof("hbm", 16 * n / (ms * 1e-3) / 1e9, "8 B float64 in + 8 B int64 out per element"),
-        "bound": "valu (PCG64 128-bit LCG step + XSL-RR + 64x64 Lemire multiply per draw)",
-        # 49.6 VALU instructions per draw: the ISA of bounded_acc_kernel's
-        # 16-draw loop body (793 VALU), 14 of them half-rate 32x32->64
-        # multiplies (tools/valu_rates.hip: mad_u64 at ~0.57x the add rate)
-        "roofline_valu": roof("valu", 10 * n / (ms * 1e-3) * 49.6 / 1e9,
-                              "49.6 VALU instructions per draw (ISA count), 10 draws per element"),
-        "numpy_prefix_equal": ok,
-        "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}
+    rows["mask_masking"] = mask_row(dev, log2n)
     return rows
 
 

@@ -15,6 +15,8 @@ out = {}
 for r in os.environ.get("ROWS", "byte_api,draw_split").split(","):
     if r == "byte_api":
         out[r] = bench.byte_api_row()
+    elif r == "mask":
+        out[r] = bench.mask_row(dev, int(os.environ.get("LOG2N", "24")))
     elif r == "draw_split":
         out[r] = bench.draw_split_row(dev, int(os.environ.get("LOG2N", "24")))
 print(json.dumps(out))

@@ -32,3 +32,21 @@ def test_masked_result_round_over_loopback(coeffs, seal):
         e2e.stop_peer(proc, port)
     assert st["peer_verified"]
     assert st["bytes_posted"] > 5 * 66 * (1 << 14) * (2.6 if seal else 1)
+
+
+@pytest.mark.gpu
+def test_masked_result_round_full_size():
+    """BASELINE config 5 at its own size: 2^24 int64 elements, MT19937
+    coefficients in the reference's order (make_shares_vec, the drop-in path),
+    every share vector posted to the peer, which reconstructs from shares 1, 3,
+    5 and verifies the digest of the secrets."""
+    e2e = _e2e()
+    port = 21000 + os.getpid() % 1000
+    proc = e2e.start_peer(port)
+    try:
+        e2e._wait_ready(port)
+        st = e2e.run_round(1 << 24, port, coeffs="mt", seed=7, seal=False)
+    finally:
+        e2e.stop_peer(proc, port)
+    assert st["peer_verified"]
+    assert st["bytes_posted"] > 5 * 66 * (1 << 24)
