@@ -358,6 +358,9 @@ def envelope_row(recs, reps: int, s, e) -> dict:
     return row
 
 
+MASK_MIX_BOUND = 1.0 / (23.5 / 3.6e13 + 22.0 / 6.1e13)  # draws/s the draw loop's instruction mix allows
+
+
 def mask_row(dev, log2n: int) -> dict:
     """mask PRG + fixed-point masking = fix_precision(val) + seed mask + 9
     pairwise masks (runner/horizontal/agg.py:284-318 with |u2| = 10), one
@@ -400,12 +403,17 @@ def mask_row(dev, log2n: int) -> dict:
         "workload": f"fix_precision(2^{log2n} float64) + 10 make_mask(32-byte seed) with signs, int64",
         "ms": ms, "elems_per_s": n / (ms * 1e-3), "draws_per_s": 10 * n / (ms * 1e-3),
         "roofline": roof("hbm", 16 * n / (ms * 1e-3) / 1e9, "8 B float64 in + 8 B int64 out per element"),
-        "bound": "valu (PCG64 128-bit LCG step + XSL-RR + 64x64 Lemire multiply per draw)",
-        # 49.6 VALU instructions per draw: the ISA of bounded_acc_kernel's
-        # 16-draw loop body (793 VALU), 14 of them half-rate 32x32->64
-        # multiplies (tools/valu_rates.hip: mad_u64 at ~0.57x the add rate)
-        "roofline_valu": roof("valu", 10 * n / (ms * 1e-3) * 49.6 / 1e9,
-                              "49.6 VALU instructions per draw (ISA count), 10 draws per element"),
+        "bound": "valu (PCG64 128-bit LCG step + XSL-RR + Lemire per draw)",
+        # ISA of bounded_acc_kernel<true>'s paired-generator loop body (2 x 8
+        # draws): 45.5 VALU per draw, 23.5 of them VOP3 (v_mad_u64_u32,
+        # v_mul_lo_u32, 64-bit shifts / adds) and 22 VOP1/VOP2; measured issue
+        # rates (tools/valu_rates.hip): VOP3 3.6e13, VOP1/2 6.1e13
+        # lane-ops/s -> the mix allows 1 / (23.5 / 3.6e13 + 22 / 6.1e13) draws/s
+        "roofline_valu": roof("valu", 10 * n / (ms * 1e-3) * 45.5 / 1e9,
+                              "45.5 VALU instructions per draw (ISA count), 10 draws per element"),
+        "mix_bound": {"draws_per_s": MASK_MIX_BOUND, "frac": 10 * n / (ms * 1e-3) / MASK_MIX_BOUND,
+                      "per_draw": "23.5 VOP3 @ 3.6e13/s + 22 VOP1/2 @ 6.1e13/s (draw loop only; tile jumps, "
+                                  "base conversion and stores are extra instructions)"},
         "numpy_prefix_equal": ok,
         "cpu_numpy": {"elems_per_s": m / cpu_dt, "sample": f"2^20 elements x 10 masks, numpy 1 thread"}}
 

@@ -7,12 +7,17 @@
 // LCG s' = a s + inc jumps ahead in closed form, s_r = A_r s_0 + inc G_r with
 // A_r = a^r, G_r = 1 + a + ... + a^(r-1) (mod 2^128).  So lanes generate
 // their elements independently: lane l of a wave owns elements
-// e0 + l + 64 i; it jumps once to raw e0 + l and then steps by 64 with the
-// constant map (A_64, inc G_64).  Consecutive lanes write consecutive int64s
-// (512 B per wave store).  The output equals numpy's whenever no raw draw in
-// the range is rejected by Lemire's test (odds 2^-47 per draw for make_mask);
-// every draw is tested and rejections are counted per generator, and the
-// caller then replays that generator exactly with per-segment raw offsets.
+// e0 + l + 64 i and steps by 64 with the constant map (A_64, inc G_64).  A
+// wave tile's start states cost ONE jump: lane g jumps generator g (all
+// generators at once), each lane then applies its fixed T^lane.  Generators
+// are sorted by sign on the host and drawn in pairs (two independent LCG
+// chains per lane); make_mask's Lemire range 2^47 - 1 takes the product
+// x (2^47 - 1) as a shift and a subtraction.  Consecutive lanes write
+// consecutive int64s (512 B per wave store).  The output equals numpy's
+// whenever no raw draw in the range is rejected by Lemire's test (odds 2^-47
+// per draw for make_mask); every draw is tested and rejections are counted per
+// generator, and the caller then replays that generator exactly with
+// per-segment raw offsets.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -24,10 +29,11 @@
 namespace dn {
 
 constexpr int kMaskBlock = 256;
-constexpr int kDrawsPerLane = 16;                // per chunk
-constexpr int kChunkElems = 64 * kDrawsPerLane;  // 1024
-constexpr int kChunks = 4;
+constexpr int kDrawsPerLane = 8;                 // per chunk
+constexpr int kChunkElems = 64 * kDrawsPerLane;  // 512
+constexpr int kChunks = 8;
 constexpr uint64_t kTileElems = kChunkElems * kChunks;  // 4096 per wave tile
+constexpr int kMersK = 47;  // make_mask's integers(0, 2**47 - 1): Lemire range 2^47 - 1
 
 struct AccArgs {
   int64_t* out;
@@ -36,9 +42,11 @@ struct AccArgs {
   double scale;
   uint64_t elem_begin, elem_end;
   uint64_t excl, threshold;
-  int64_t low;
+  uint64_t low_total;  // sum_g sign_g * low (mod 2^64), added once per element
+  int32_t mers_k;      // excl == 2^mers_k - 1 (make_mask: 47), else 0 (general multiply)
   int32_t ngen;
-  int32_t sign[DN_MASK_MAX_GENS];
+  int32_t npos;                   // generators [0, npos) add, [npos, ngen) subtract
+  int32_t orig[DN_MASK_MAX_GENS]; // caller's index of each (sign-sorted) generator
   uint64_t raw_off[DN_MASK_MAX_GENS];
   u128 state0[DN_MASK_MAX_GENS];  // state before raw draw 0 (draw r uses T^(r+1))
   u128 inc[DN_MASK_MAX_GENS];
@@ -61,34 +69,84 @@ __device__ __forceinline__ int64_t f64_to_i64_x86(double x) {
   return static_cast<int64_t>(x);
 }
 
-// (A, G) of T^r for a wave-uniform r: product of the set bits' tables.
-__device__ __forceinline__ void jump_uniform(const AccArgs& a, uint64_t r, u128& A, u128& G) {
-  A = 1;
-  G = 0;
-  for (int k = 0; k < 64 && (r >> k); ++k) {
-    if ((r >> k) & 1u) {
-      G = a.jA[k] * G + a.jG[k];
-      A = a.jA[k] * A;
-    }
-  }
+__device__ __forceinline__ u128 bcast_u128(u128 v, int src) {  // v of lane `src` (wave-uniform src)
+  const uint64_t lo = static_cast<uint64_t>(v), hi = static_cast<uint64_t>(v >> 64);
+  const uint32_t w0 = __builtin_amdgcn_readlane(static_cast<uint32_t>(lo), src);
+  const uint32_t w1 = __builtin_amdgcn_readlane(static_cast<uint32_t>(lo >> 32), src);
+  const uint32_t w2 = __builtin_amdgcn_readlane(static_cast<uint32_t>(hi), src);
+  const uint32_t w3 = __builtin_amdgcn_readlane(static_cast<uint32_t>(hi >> 32), src);
+  return to_u128((static_cast<uint64_t>(w3) << 32) | w2, (static_cast<uint64_t>(w1) << 32) | w0);
 }
 
-// ... composed with T^l for the lane offset l < 64 (6 predicated steps).
-__device__ __forceinline__ void jump_lane(const AccArgs& a, uint32_t l, u128& A, u128& G) {
+// kDrawsPerLane draws of K generators (same sign) at stride 64 (lane-strided
+// elements), accumulated into acc.  K = 2 interleaves two independent LCG
+// chains for latency hiding.  Lemire's value is the high word of x * excl; for
+// excl = 2^k - 1 that is x 2^k - x (shifts, no multiply).  The rejection test
+// (low word < threshold) also covers draws past elem_end: a spurious hit (odds
+// 2^-47 per draw) only sends the generator down the exact replay path.
+// Returns bit j set if generator j saw a rejected draw.
+template <bool MERS>
+__device__ __forceinline__ uint64_t lemire_hi(const uint64_t x, const uint64_t excl, const uint64_t thr, bool& rj) {
+  uint64_t lo, hi;
+  if (MERS) {
+    const uint64_t xs = x << kMersK;
+    lo = xs - x;
+    hi = (x >> (64 - kMersK)) - (xs < x ? 1u : 0u);
+  } else {
+    const u128 m = static_cast<u128>(x) * excl;
+    lo = static_cast<uint64_t>(m);
+    hi = static_cast<uint64_t>(m >> 64);
+  }
+  rj |= lo < thr;
+  return hi;
+}
+
+template <bool MERS, bool NEG, int K>
+__device__ __forceinline__ uint32_t draws_chunk(u128 (&st)[K], uint64_t (&acc)[kDrawsPerLane], const u128 A64,
+                                                const u128 (&c64)[K], const uint64_t excl, const uint64_t thr) {
+  bool rj[K];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    if ((l >> k) & 1u) {
-      G = a.jA[k] * G + a.jG[k];
-      A = a.jA[k] * A;
+  for (int j = 0; j < K; ++j) rj[j] = false;
+#pragma unroll
+  for (int i = 0; i < kDrawsPerLane; ++i) {
+    uint64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      sum += lemire_hi<MERS>(xsl_rr(st[j]), excl, thr, rj[j]);
+      st[j] = A64 * st[j] + c64[j];
     }
+    acc[i] = NEG ? acc[i] - sum : acc[i] + sum;
   }
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) m |= rj[j] ? (1u << j) : 0u;
+  return m;
 }
 
-// Each lane keeps one PCG64 state per generator; they live in LDS between
-// chunks (16 B per lane per generator, wave-private slots, no barrier) so
-// that the generator loop can stay a runtime loop at ~60 VGPRs.
+// One step of the generator loop: generators [g, g + K) of one sign.
+template <bool MERS, bool NEG, int K>
+__device__ __forceinline__ uint32_t gens_step(const AccArgs& a, u128* s_state, const uint32_t tid, const int g,
+                                              uint64_t (&acc)[kDrawsPerLane]) {
+  u128 st[K], c[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    st[j] = s_state[(g + j) * kMaskBlock + tid];
+    c[j] = a.c64[g + j];
+  }
+  const uint32_t m = draws_chunk<MERS, NEG, K>(st, acc, a.A64, c, a.excl, a.threshold);
+#pragma unroll
+  for (int j = 0; j < K; ++j) s_state[(g + j) * kMaskBlock + tid] = st[j];
+  return m << g;
+}
+
+// Each lane keeps one PCG64 state per generator in LDS between chunks (16 B
+// per lane per generator, wave-private slots, no barrier; dynamic LDS sized by
+// ngen).  A tile's start states come from ONE lane-parallel jump: lane g < ngen
+// jumps generator g to the tile start (all generators' jumps in the time of
+// one), each lane then offsets itself by its fixed T^lane.
+template <bool MERS>
 __global__ void __launch_bounds__(kMaskBlock) bounded_acc_kernel(const AccArgs a) {
-  __shared__ u128 s_state[DN_MASK_MAX_GENS][kMaskBlock];
+  extern __shared__ u128 s_state[];  // [ngen][kMaskBlock]
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
   const uint64_t n = a.elem_end - a.elem_begin;
@@ -98,59 +156,90 @@ __global__ void __launch_bounds__(kMaskBlock) bounded_acc_kernel(const AccArgs a
   uint32_t rejmask = 0u;  // bit g: this lane saw a rejected draw of generator g
   for (uint64_t tile = wave0; tile < ntiles; tile += nwaves) {
     const uint64_t e0 = a.elem_begin + tile * kTileElems;  // wave-uniform
+    if (a.ngen > 0) {
+      // (recomputed per tile rather than held in registers across the draw loops)
+      // this lane's generator for the tile-start jump (lanes >= ngen idle there)
+      uint64_t my_off = 0;
+      u128 my_s0 = 0, my_inc = 0;
 #pragma unroll 1
-    for (int g = 0; g < a.ngen; ++g) {
-      u128 A, G;
-      jump_uniform(a, a.raw_off[g] + e0 + 1, A, G);  // raw r needs T^(r+1) from state0
-      jump_lane(a, lane, A, G);
-      s_state[g][tid] = A * a.state0[g] + a.inc[g] * G;
+      for (int g = 0; g < a.ngen; ++g) {
+        if (lane == static_cast<uint32_t>(g)) {
+          my_off = a.raw_off[g];
+          my_s0 = a.state0[g];
+          my_inc = a.inc[g];
+        }
+      }
+      const uint64_t r = my_off + e0 + 1;  // raw draw r needs T^(r+1) from state0
+      u128 A = 1, G = 0;
+#pragma unroll 1
+      for (int k = 0; k < 64; ++k) {
+        const uint64_t rk = r >> k;
+        if (!__any(rk != 0)) break;
+        if (rk & 1u) {
+          G = a.jA[k] * G + a.jG[k];
+          A = a.jA[k] * A;
+        }
+      }
+      const u128 s_tile = A * my_s0 + my_inc * G;
+      // T^lane = (A_l, G_l)
+      u128 Al = 1, Gl = 0;
+#pragma unroll 1
+      for (int k = 0; k < 6; ++k) {
+        if ((lane >> k) & 1u) {
+          Gl = a.jA[k] * Gl + a.jG[k];
+          Al = a.jA[k] * Al;
+        }
+      }
+#pragma unroll 1
+      for (int g = 0; g < a.ngen; ++g)
+        s_state[g * kMaskBlock + tid] = Al * bcast_u128(s_tile, g) + a.inc[g] * Gl;
     }
+    const bool full = e0 + kTileElems <= a.elem_end;
 #pragma unroll 1
     for (int c = 0; c < kChunks; ++c) {
       const uint64_t ec = e0 + static_cast<uint64_t>(c) * kChunkElems + lane;
       uint64_t acc[kDrawsPerLane];
-#pragma unroll
-      for (int i = 0; i < kDrawsPerLane; ++i) {
-        const uint64_t e = ec + 64u * i;
-        uint64_t v = 0;
-        if (e < a.elem_end) {
-          if (a.base_i64) v = static_cast<uint64_t>(a.base_i64[e]);
-          else if (a.base_f64) v = static_cast<uint64_t>(f64_to_i64_x86(a.base_f64[e] * a.scale));
-        }
-        acc[i] = v;
-      }
-#pragma unroll 1
-      for (int g = 0; g < a.ngen; ++g) {
-        const bool neg = a.sign[g] < 0;
-        const u128 c64 = a.c64[g];
-        u128 st = s_state[g][tid];
-        bool rj = false;
+      if (a.base_i64) {  // base kind and tile fullness are wave-uniform: no per-element branches
 #pragma unroll
         for (int i = 0; i < kDrawsPerLane; ++i) {
-          const uint64_t x = xsl_rr(st);
-          const u128 m = static_cast<u128>(x) * a.excl;
-          const uint64_t val = static_cast<uint64_t>(a.low) + static_cast<uint64_t>(m >> 64);
-          rj |= ((ec + 64u * i) < a.elem_end) && (static_cast<uint64_t>(m) < a.threshold);
-          acc[i] = neg ? acc[i] - val : acc[i] + val;
-          st = a.A64 * st + c64;
+          const uint64_t e = ec + 64u * i;
+          acc[i] = (full || e < a.elem_end) ? static_cast<uint64_t>(a.base_i64[e]) : 0u;
         }
-        s_state[g][tid] = st;
-        if (rj) rejmask |= 1u << g;
+      } else if (a.base_f64) {
+#pragma unroll
+        for (int i = 0; i < kDrawsPerLane; ++i) {
+          const uint64_t e = ec + 64u * i;
+          acc[i] = (full || e < a.elem_end) ? static_cast<uint64_t>(f64_to_i64_x86(a.base_f64[e] * a.scale)) : 0u;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kDrawsPerLane; ++i) acc[i] = 0;
       }
+#pragma unroll
+      for (int i = 0; i < kDrawsPerLane; ++i) acc[i] += a.low_total;
+      // generators are sorted by sign on the host (positives first), so pairs share a sign
+      int g = 0;
+#pragma unroll 1
+      for (; g + 1 < a.npos; g += 2) rejmask |= gens_step<MERS, false, 2>(a, s_state, tid, g, acc);
+      if (g < a.npos) rejmask |= gens_step<MERS, false, 1>(a, s_state, tid, g++, acc);
+#pragma unroll 1
+      for (; g + 1 < a.ngen; g += 2) rejmask |= gens_step<MERS, true, 2>(a, s_state, tid, g, acc);
+      if (g < a.ngen) rejmask |= gens_step<MERS, true, 1>(a, s_state, tid, g, acc);
 #pragma unroll
       for (int i = 0; i < kDrawsPerLane; ++i) {
         const uint64_t e = ec + 64u * i;
-        if (e < a.elem_end) __builtin_nontemporal_store(static_cast<int64_t>(acc[i]), a.out + e);
+        if (full || e < a.elem_end) __builtin_nontemporal_store(static_cast<int64_t>(acc[i]), a.out + e);
       }
     }
   }
   if (a.rejects) {
 #pragma unroll 1
     for (int g = 0; g < a.ngen; ++g) {
-      if (__ballot((rejmask >> g) & 1u) && lane == 0) atomicAdd(a.rejects + g, 1u);
+      if (__ballot((rejmask >> g) & 1u) && lane == 0) atomicAdd(a.rejects + a.orig[g], 1u);
     }
   }
 }
+
 
 struct RejArgs {
   u128 state0, inc, c64;
@@ -239,23 +328,33 @@ extern "C" int dn_bounded_i64_accumulate(const dn_pcg64_t* gens, const int32_t* 
   a.elem_end = elem_end;
   a.excl = rng + 1;
   a.threshold = (~0ull - rng) % a.excl;
-  a.low = low;
   a.ngen = ngen;
   a.rejects = reject_count;
   pcg64_jump_tables(a.jA, a.jG);
   a.A64 = a.jA[6];
-  for (int g = 0; g < ngen; ++g) {
+  for (int g = 0; g < ngen; ++g)
     if (signs[g] != 1 && signs[g] != -1) return set_error(DN_ERR_ARG, "dn_bounded_i64_accumulate: sign must be +-1");
-    a.sign[g] = signs[g];
-    a.raw_off[g] = raw_offsets ? raw_offsets[g] : 0;
-    a.state0[g] = to_u128(gens[g].state_hi, gens[g].state_lo);
-    a.inc[g] = to_u128(gens[g].inc_hi, gens[g].inc_lo);
-    a.c64[g] = a.inc[g] * a.jG[6];
+  int slot = 0;
+  for (int pass = 0; pass < 2; ++pass) {  // positives first, then negatives (the sum commutes)
+    for (int g = 0; g < ngen; ++g) {
+      if ((signs[g] < 0) != (pass == 1)) continue;
+      a.orig[slot] = g;
+      a.low_total += signs[g] < 0 ? 0ull - static_cast<uint64_t>(low) : static_cast<uint64_t>(low);
+      a.raw_off[slot] = raw_offsets ? raw_offsets[g] : 0;
+      a.state0[slot] = to_u128(gens[g].state_hi, gens[g].state_lo);
+      a.inc[slot] = to_u128(gens[g].inc_hi, gens[g].inc_lo);
+      a.c64[slot] = a.inc[slot] * a.jG[6];
+      ++slot;
+    }
+    if (pass == 0) a.npos = slot;
   }
   const uint64_t tiles = (elem_end - elem_begin + kTileElems - 1) / kTileElems;
   const dim3 grid(grid_for_tiles(tiles)), block(kMaskBlock);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(bounded_acc_kernel, grid, block, 0, s, a);
+  if (a.excl == (1ull << kMersK) - 1) a.mers_k = kMersK;  // Lemire by shifts (make_mask's range)
+  const size_t lds = static_cast<size_t>(ngen) * kMaskBlock * sizeof(u128);
+  if (a.mers_k) hipLaunchKernelGGL(bounded_acc_kernel<true>, grid, block, lds, s, a);
+  else hipLaunchKernelGGL(bounded_acc_kernel<false>, grid, block, lds, s, a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_bounded_i64_accumulate: %s", hipGetErrorString(err));
   return DN_OK;

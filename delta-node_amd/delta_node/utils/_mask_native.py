@@ -6,7 +6,7 @@ from typing import List, Optional, Sequence, Union
 
 from ..crypto.shamir import _native
 
-MAX_GENS = 8
+MAX_GENS = 16
 EXPORTS = ("dn_pcg64_seed", "dn_pcg64_advance", "dn_bounded_i64_accumulate", "dn_bounded_i64_rejects",
            "dn_unfix_precision", "dn_i64_sum")
 

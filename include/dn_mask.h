@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DN_MASK_MAX_GENS 8
+#define DN_MASK_MAX_GENS 16
 
 /* A PCG64 generator: 128-bit state and increment (numpy's PCG64.state). */
 typedef struct dn_pcg64 {

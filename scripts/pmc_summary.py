@@ -21,14 +21,22 @@ vals = defaultdict(lambda: defaultdict(list))
 for name in ("pmc_fetch", "pmc_write", "pmc_req"):
     with open(f"{d}/{name}.csv") as f:
         for row in csv.DictReader(f):
-            k = "split" if "split_kernel" in row["Kernel_Name"] else (
-                "reconstruct" if "reconstruct_kernel" in row["Kernel_Name"] else None)
+            kn = row["Kernel_Name"]
+            k = ("split" if "split_kernel" in kn else
+                 "reconstruct" if "reconstruct_kernel" in kn else
+                 "fused_draw_split" if "mt_gen_kernel<3>" in kn else
+                 "mask_accumulate" if "bounded_acc_kernel" in kn else None)
             if k:
                 vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-alg = {"split": N * (8 + 2 * 66 + 5 * 66), "reconstruct": N * (3 * 66 + 8)}
-alg_rw = {"split": (N * (8 + 2 * 66), N * 5 * 66), "reconstruct": (N * 3 * 66, N * 8)}
-res = {"N": N, "workload": "3-of-5 split / reconstruct xs=1,3,5 -> int64, 2^24 elements", "kernels": {}}
+alg = {"split": N * (8 + 2 * 66 + 5 * 66), "reconstruct": N * (3 * 66 + 8),
+       "fused_draw_split": N * (8 + 5 * 66), "mask_accumulate": N * 16}
+alg_rw = {"split": (N * (8 + 2 * 66), N * 5 * 66), "reconstruct": (N * 3 * 66, N * 8),
+          "fused_draw_split": (N * 8, N * 5 * 66), "mask_accumulate": (N * 8, N * 8)}
+res = {"N": N, "workload": "3-of-5 split / reconstruct xs=1,3,5 -> int64, 2^24 elements; fused MT draw + split "
+                     "(make_shares_vec); mask accumulate (10 generators, float64 base)", "kernels": {}}
 for k, c in vals.items():
+    if not c.get("FETCH_SIZE") or not c.get("WRITE_SIZE") or not c.get("TCC_EA0_RDREQ_sum"):
+        continue
     fetch = statistics.median(c["FETCH_SIZE"]) * 1024
     write = statistics.median(c["WRITE_SIZE"]) * 1024
     rdreq = statistics.median(c["TCC_EA0_RDREQ_sum"])

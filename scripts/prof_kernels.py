@@ -38,3 +38,18 @@ for _ in range(reps):
 torch.cuda.synchronize()
 assert torch.equal(rec, sec)
 print("ok", reps, "x split + reconstruct of", N)
+if os.environ.get("EXTRA", "1") == "1":
+    # the fused bit-exact draw + split (make_shares_vec's default: mt_gen_kernel<3>)
+    # and the mask row (bounded_acc_kernel, 10 generators, fixed-point base)
+    from delta_node.utils import masked_sum  # noqa: E402
+
+    del coeffs
+    for i in range(reps):
+        ss.make_shares_vec(sec, 5, out=shares)
+    val = torch.randn(N, dtype=torch.float64, device=dev)
+    terms = [(bytes([i]) * 32, 1 if i % 2 else -1) for i in range(10)]
+    out = torch.empty(N, dtype=torch.int64, device=dev)
+    for _ in range(reps):
+        masked_sum(val, terms, precision=8, out=out)
+    torch.cuda.synchronize()
+    print("ok", reps, "x fused draw+split and mask row of", N)
