@@ -44,7 +44,8 @@ def encode_share_vec(vec, n: int, x: int, *, trim: bool = True):
     dev = vec.device
     cap = int(L.dn_m521_encoded_capacity(n, x))
     out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
-    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    # every entry is written by the encoder (offsets[n] by the last element)
+    offsets = torch.empty(n + 1, dtype=torch.int64, device=dev) if n else torch.zeros(1, dtype=torch.int64, device=dev)
     sb = int(L.dn_m521_codec_scratch_bytes(n))
     scratch = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
     _native.check(L.dn_m521_encode_shares(vec.data_ptr(), n, x, offsets.data_ptr(), out.data_ptr(), cap,
