@@ -5,22 +5,23 @@
 // 1 + getrandbits(521), redrawn while >= p-1; getrandbits(521) is 17 MT19937
 // words, little-endian, the last >> 23.  dn_mt19937_draw_coeffs (host_m521.cpp)
 // restates that stream sequentially; this file produces the same values on the
-// device by cutting the word stream into S substreams of L = 17 * 2^15 words
-// (2^15 whole draws each), all on the GPU:
+// device by cutting the word stream into S substreams of L = 17 * 2^14 words
+// (2^14 whole draws each), all on the GPU:
 //
-//  * jump kernels: the MT window at the start of every substream by
+//  * jump kernel: the MT window at the start of every substream by
 //    jump-ahead, g(f)(W) with g = x^J mod P (P the characteristic polynomial
-//    of the one-word transition f; tools/gen_mt_jump.py), evaluated by
-//    Horner over 4-bit chunks of g: r <- f^4(r) ^ T[chunk], T the 16
-//    combinations of f^0..f^3(W) in LDS.  A wave holds r (624 words + 16 free
-//    slots) in 10 VGPRs; f^4 appends 4 words (readlane -> scalar twist ->
-//    writelane).  Windows are at most three jumps (radix-64 digits of s - 1,
-//    mt19937_jump.inc) from the caller's window: one launch per level, every
-//    jump of a level independent;
-//  * generation kernel: one wave per substream keeps its window in LDS,
-//    twists it (CPython's three dependency phases, up to 4 words per lane),
-//    tempers into an LDS ring and turns every 17-word group into one
-//    coefficient (+1, rejection test) stored in the tiled layout; one extra
+//    of the one-word transition f; tools/gen_mt_jump.py), evaluated by Horner
+//    over 64-bit chunks of g: r <- f^64(r) ^ sum of table rows, the table E the
+//    64 combinations of six consecutive shifts of W, in LDS.  A wave holds r
+//    (624 words + 80 free slots) in 11 VGPRs; f^64 appends 64 words (three
+//    ds_bpermute + the twist per lane).  Windows are at most three jumps
+//    (radix-64 digits of s - 1, mt19937_jump.inc) from the caller's window:
+//    one launch per level, every jump of a level independent;
+//  * generation kernel: one wave per substream keeps its window in the same
+//    register ring, appends 64 words at a time, tempers them into an LDS ring
+//    and turns every 17-word group into one coefficient (+1, rejection test):
+//    stored in the tiled layout (T = 0) or consumed at once by the split of
+//    the element it belongs to (T = t, the fused draw + split); one extra
 //    wave steps the last window before CPython's final array to it, so
 //    self.random continues exactly as after n sequential make_shares calls.
 // A rejected draw (probability ~2^-520 per coefficient) shifts every later
