@@ -315,8 +315,14 @@ __device__ __forceinline__ void gen_run(uint32_t (&Q)[11], const Lanes& L, uint3
 // their int64 secrets, and the split of split_kernel<T, false, false>: the
 // forward-difference table stored share by share.
 template <int T>
-__device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t e, uint32_t lane) {
+__device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t ebase, uint32_t lane) {
   constexpr int TM1 = T - 1;
+  // ebase (the group's first element) is wave-uniform and a multiple of 64, so
+  // the group's 64 elements share one tile: its index is a scalar and every
+  // share store takes the tile's buffer descriptor from SGPRs (no per-lane
+  // descriptor, no waterfall loop around the stores)
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ebase >> 8));
+  const uint64_t e = ebase + lane;
   if (e >= a.n_elem) return;
   uint32_t c[T][kLimbs];
   const uint32_t* w = rb + 17u * TM1 * lane;
@@ -339,7 +345,7 @@ __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb,
 #pragma unroll
   for (int i = 2; i < kLimbs; ++i) c[0][i] = 0u;
   fd_init<T>(c);
-  const uint32_t tile = static_cast<uint32_t>(e >> 8), wl = static_cast<uint32_t>(e & 255u);
+  const uint32_t wl = static_cast<uint32_t>(e & 255u);
 #pragma unroll 1
   for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
     store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vb, tile)), wl, c[0]);
@@ -416,7 +422,7 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
       if constexpr (T == 0) {
         emit_group(a, rb, qb, rbm, 64u * done + lane, nloc, lane);
       } else {
-        emit_split<T>(a, rb, qb + 64u * done + lane, lane);  // k0 / (t-1) = the substream's first element
+        emit_split<T>(a, rb, qb + 64u * done, lane);  // k0 / (t-1) = the substream's first element
       }
       ++done;
     }
