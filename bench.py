@@ -123,29 +123,23 @@ def c_port_baseline(t: int, n: int, xs, budget_s: float, threads: int) -> dict:
                       f"n={n} + reconstruct xs={list(xs)}), C restatement, {wall:.1f} s wall"}
 
 
-def measure_ceiling(dev, sec, coeffs, shares, N: int, t: int, n: int, reps: int = 5) -> dict:
-    """Same-buffer HBM ceiling of the split (lib/libdn_diag.so,
-    dn_diag_tile_stream): the split's exact bytes per tile — the rank's
-    secrets, t-1 coefficient rows read, n share rows written — over the SAME
-    buffers (so the same physical pages, whose placement sets this part's
-    write rate: DESIGN.md §5.1), with 16-B non-temporal accesses and no
-    arithmetic; the fastest of four grid sizes.  Overwrites `shares`."""
+def stream_ceiling(ins, in_bpt, outs, out_bpt, ntiles: int, reps: int = 5) -> dict:
+    """dn_diag_tile_stream (lib/libdn_diag.so): per tile, 16-B non-temporal
+    loads of `in_bpt[i]` bytes from every input buffer, then 16-B stores of
+    `out_bpt[j]` bytes to every output buffer, no arithmetic; the fastest of
+    four grid sizes.  Overwrites the outputs."""
     import ctypes
-
-    from delta_node.crypto.shamir import field
 
     diag = ctypes.CDLL(os.path.join(ROOT, "delta-node_amd", "lib", "libdn_diag.so"))
     vp = ctypes.c_void_p
-    if N % field.TILE:
-        return None
-    ins = (vp * 8)(sec.data_ptr(), *[coeffs[j].data_ptr() for j in range(t - 1)])
-    ibpt = (ctypes.c_uint32 * 8)(8 * field.TILE, *([field.TILE_BYTES] * (t - 1)))
-    outs = (vp * 16)(*[shares[x].data_ptr() for x in range(n)])
-    obpt = (ctypes.c_uint32 * 16)(*([field.TILE_BYTES] * n))
+    ip = (vp * 16)(*[t.data_ptr() for t in ins])
+    ib = (ctypes.c_uint32 * 16)(*in_bpt)
+    op = (vp * 16)(*[t.data_ptr() for t in outs])
+    ob = (ctypes.c_uint32 * 16)(*out_bpt)
     stream = torch.cuda.current_stream()
 
     def launch(grid):
-        rc = diag.dn_diag_tile_stream(ins, ibpt, t, outs, obpt, n, ctypes.c_uint64(N // field.TILE), grid,
+        rc = diag.dn_diag_tile_stream(ip, ib, len(ins), op, ob, len(outs), ctypes.c_uint64(ntiles), grid,
                                       vp(stream.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"dn_diag_tile_stream rc={rc}")
@@ -162,8 +156,35 @@ def measure_ceiling(dev, sec, coeffs, shares, N: int, t: int, n: int, reps: int 
         ms = s.elapsed_time(e) / reps
         if best is None or ms < best["ms"]:
             best = {"ms": ms, "grid": grid}
+    return best
+
+
+def measure_ceiling(dev, sec, coeffs, shares, N: int, t: int, n: int, reps: int = 5) -> dict:
+    """Same-buffer HBM ceiling of the split: the split's exact bytes per tile —
+    the rank's secrets, t-1 coefficient rows read, n share rows written — over
+    the SAME buffers (so the same physical pages, whose placement sets this
+    part's write rate: DESIGN.md §5.1).  Overwrites `shares`."""
+    from delta_node.crypto.shamir import field
+
+    if N % field.TILE:
+        return None
+    best = stream_ceiling([sec] + [coeffs[j] for j in range(t - 1)], [8 * field.TILE] + [field.TILE_BYTES] * (t - 1),
+                          [shares[x] for x in range(n)], [field.TILE_BYTES] * n, N // field.TILE, reps)
     best["kernel"] = ("dn_diag_tile_stream: the split's bytes over the same buffers, 16-B nt loads then stores "
                       "per tile, no arithmetic (fastest of grids 256/1024/4096/16384)")
+    return best
+
+
+def measure_recon_ceiling(share_rows, rec, N: int, reps: int = 5) -> dict:
+    """Same-buffer ceiling of the reconstruct: its k share rows read, the int64
+    output written, per tile, over the same buffers.  Overwrites `rec`."""
+    from delta_node.crypto.shamir import field
+
+    if N % field.TILE:
+        return None
+    best = stream_ceiling(list(share_rows), [field.TILE_BYTES] * len(share_rows), [rec], [8 * field.TILE],
+                          N // field.TILE, reps)
+    best["kernel"] = "dn_diag_tile_stream: the reconstruct's bytes over the same buffers, no arithmetic"
     return best
 
 
@@ -829,6 +850,7 @@ def main():
 
     # ---- same-buffer ceiling: the split's bytes through the same pages -----
     ceiling = measure_ceiling(dev, sec, coeffs, shares, N, t, n) if N >= (1 << 20) else None
+    recon_ceiling = measure_recon_ceiling(share_rows, rec, N) if N >= (1 << 20) else None
 
     # ---- N > 1: the weak-scaling figure (2^log2n elements per GPU) --------
     weak = None
@@ -908,7 +930,10 @@ def main():
                          "split_frac_of_ceiling": ceiling["ms"] / split_ms}},
         "kernels": {"split_ms": split_ms, "reconstruct_ms": recon_ms,
                     "split_GBps": achieved, "reconstruct_GBps": recon_bytes / (recon_ms * 1e-3) / 1e9,
-                    "split_elems_per_s": N / (split_ms * 1e-3), "reconstruct_elems_per_s": N / (recon_ms * 1e-3)},
+                    "split_elems_per_s": N / (split_ms * 1e-3), "reconstruct_elems_per_s": N / (recon_ms * 1e-3),
+                    "reconstruct_ceiling_measured": recon_ceiling and {
+                        **recon_ceiling, "GBps": recon_bytes / (recon_ceiling["ms"] * 1e-3) / 1e9,
+                        "reconstruct_frac_of_ceiling": recon_ceiling["ms"] / recon_ms}},
         "parity": {"roundtrip_equal": roundtrip, "c_oracle_sample_equal": oracle_ok, "sample": sample,
                    "all_ranks_ok": all_ok},
     }
