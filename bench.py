@@ -472,19 +472,56 @@ def rows_bench(dev, log2n: int) -> dict:
     blk = ss.make_shares_vec(torch.from_numpy(secrets_int64(3, n)), 5)
     packed, offs = codec.encode_share_vec(blk[2], n, 3)
     torch.cuda.synchronize()
+    # the API calls (allocation of the outputs, the decoder's bad-record read-back included)
     s.record()
     for _ in range(reps):
         packed, offs = codec.encode_share_vec(blk[2], n, 3, trim=False)
     e.record()
     torch.cuda.synchronize()
-    enc_ms = s.elapsed_time(e) / reps
+    enc_call_ms = s.elapsed_time(e) / reps
     total = int(offs[n].item())
     s.record()
     for _ in range(reps):
         vec, _xs = codec.decode_share_vec(packed, offs, n)
     e.record()
     torch.cuda.synchronize()
-    dec_ms = s.elapsed_time(e) / reps
+    dec_call_ms = s.elapsed_time(e) / reps
+    # the kernels: the C entry points on preallocated buffers, events on their stream
+    import ctypes as _ct
+
+    CL = codec._lib()
+    cap = int(CL.dn_m521_encoded_capacity(n, 3))
+    kout = torch.empty(cap, dtype=torch.uint8, device=dev)
+    koffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ksb = int(CL.dn_m521_codec_scratch_bytes(n))
+    kscr = torch.empty(ksb, dtype=torch.uint8, device=dev)
+    kvec = torch.empty(_field.vec_bytes(n), dtype=torch.uint8, device=dev)
+    kxs = torch.empty(n, dtype=torch.int64, device=dev)
+    kbad = torch.zeros(1, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    from delta_node.crypto.shamir import _native as _cn
+
+    def k_enc():
+        _cn.check(CL.dn_m521_encode_shares(blk[2].data_ptr(), n, 3, koffs.data_ptr(), kout.data_ptr(), cap,
+                                           kscr.data_ptr(), ksb, _ct.c_void_p(stream.cuda_stream)))
+
+    def k_dec():
+        _cn.check(CL.dn_m521_decode_shares(packed.data_ptr(), packed.numel(), offs.data_ptr(), n, kvec.data_ptr(),
+                                           kxs.data_ptr(), kbad.data_ptr(), _ct.c_void_p(stream.cuda_stream)))
+
+    kt = {}
+    for name, fn in (("enc", k_enc), ("dec", k_dec)):
+        fn()
+        s.record(stream)
+        for _ in range(reps):
+            fn()
+        e.record(stream)
+        torch.cuda.synchronize()
+        kt[name] = s.elapsed_time(e) / reps
+    enc_ms, dec_ms = kt["enc"], kt["dec"]
+    kernels_equal = (bool(torch.equal(koffs, offs)) and bool(torch.equal(kout[:total], packed[:total]))
+                     and bool(torch.equal(kvec, blk[2])) and int(kbad.item()) == 0)
+    del kout, koffs, kscr, kvec, kxs
     # CPU: the reference's per-share codec (shamir.py:28-45) restated, on a 2^16 sample of the same shares
     from oracle.py_shamir import parse_share, share_to_bytes
 
@@ -500,6 +537,10 @@ def rows_bench(dev, log2n: int) -> dict:
     dec_bytes = total + 8 * (n + 1) + n * 66 + 8 * n
     rows["share_codec"] = {"workload": f"share x=3 of 2^{log2n} elements <-> packed _share_to_bytes records",
                            "encode_ms": enc_ms, "decode_ms": dec_ms, "bytes_out": total,
+                           "encode_call_ms": enc_call_ms, "decode_call_ms": dec_call_ms,
+                           "timing": "encode_ms / decode_ms: the C entry points on preallocated buffers (kernels); "
+                                     "*_call_ms: the Python API calls, allocating their outputs",
+                           "kernels_equal_api": kernels_equal,
                            "encode_elems_per_s": n / (enc_ms * 1e-3), "decode_elems_per_s": n / (dec_ms * 1e-3),
                            "roundtrip_equal": bool(torch.equal(vec, blk[2])),
                            "reference_bytes_equal_sample": bool(

@@ -130,11 +130,15 @@ __device__ __forceinline__ void lds_put_bytes(uint8_t* sb, int32_t lo, int32_t h
     if (pos + i >= lo && pos + i < hi) sb[pos + i] = static_cast<uint8_t>(word >> (8 * i));
 }
 
+// W16: `out` is 16-B aligned, so the window is laid out from the 16-B boundary
+// at or below its start and the body goes out as 16-B stores (else 4-B ones).
+template <bool W16>
 __global__ void __launch_bounds__(kCodecBlock) encode_kernel(const uint8_t* __restrict__ vec, uint64_t n, XBytes xb,
                                                              const uint32_t* __restrict__ local,
                                                              const uint64_t* __restrict__ block_pre,
                                                              uint64_t* __restrict__ offsets, uint8_t* __restrict__ out) {
-  __shared__ uint32_t s_buf[kCodecBlock / 64][(64 * kMaxRecord + 8) / 4 + 2];
+  constexpr int kRowWords = ((64 * kMaxRecord + 8 + 16) / 4 + 2 + 3) & ~3;  // 16-B aligned rows
+  __shared__ __attribute__((aligned(16))) uint32_t s_buf[kCodecBlock / 64][kRowWords];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint64_t e = (static_cast<uint64_t>(blockIdx.x) * kCodecBlock) + threadIdx.x;
   const bool valid = e < n;
@@ -155,7 +159,7 @@ __global__ void __launch_bounds__(kCodecBlock) encode_kernel(const uint8_t* __re
   const uint32_t last = static_cast<uint32_t>(63 - __builtin_clzll(vmask));
   const uint64_t endl = off + (valid ? 1 + xb.len + ylen : 0);
   const uint64_t B = __shfl(endl, last);
-  const uint64_t A4 = A & ~3ull;
+  const uint64_t A4 = W16 ? (A & ~15ull) : (A & ~3ull);  // LDS byte 0 of the window
   uint8_t* sb = reinterpret_cast<uint8_t*>(s_buf[wv]);
   uint32_t* sw4 = s_buf[wv];
   if (valid) {
@@ -187,18 +191,28 @@ __global__ void __launch_bounds__(kCodecBlock) encode_kernel(const uint8_t* __re
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // head bytes [A, a4), aligned body [a4, b4), tail [b4, B)
-  const uint64_t a4 = (A + 3) & ~3ull, b4 = B & ~3ull;
-  if (a4 > b4) {  // the whole range sits inside one dword
+  constexpr uint64_t kAl = W16 ? 16u : 4u;
+  const uint64_t a4 = (A + kAl - 1) & ~(kAl - 1), b4 = B & ~(kAl - 1);
+  if (a4 > b4) {  // the whole range sits inside one aligned chunk
     for (uint64_t q = A + lane; q < B; q += 64) out[q] = sb[q - A4];
     return;
   }
   if (lane < a4 - A) out[A + lane] = sb[A + lane - A4];
   if (lane < B - b4) out[b4 + lane] = sb[b4 + lane - A4];
-  const uint32_t* sw = s_buf[wv];
-  uint32_t* ow = reinterpret_cast<uint32_t*>(out + a4);
-  const uint32_t base_w = static_cast<uint32_t>((a4 - A4) / 4);
-  const uint32_t nw = static_cast<uint32_t>((b4 - a4) / 4);
-  for (uint32_t q = lane; q < nw; q += 64) __builtin_nontemporal_store(sw[base_w + q], ow + q);
+  if constexpr (W16) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* sq = reinterpret_cast<const u32x4*>(s_buf[wv]);
+    u32x4* oq = reinterpret_cast<u32x4*>(out + a4);
+    const uint32_t base_q = static_cast<uint32_t>((a4 - A4) / 16);
+    const uint32_t nq = static_cast<uint32_t>((b4 - a4) / 16);
+    for (uint32_t q = lane; q < nq; q += 64) __builtin_nontemporal_store(sq[base_q + q], oq + q);
+  } else {
+    const uint32_t* sw = s_buf[wv];
+    uint32_t* ow = reinterpret_cast<uint32_t*>(out + a4);
+    const uint32_t base_w = static_cast<uint32_t>((a4 - A4) / 4);
+    const uint32_t nw = static_cast<uint32_t>((b4 - a4) / 4);
+    for (uint32_t q = lane; q < nw; q += 64) __builtin_nontemporal_store(sw[base_w + q], ow + q);
+  }
 }
 
 // Decode record e -> element e of a tiled vector (+ its x).  y is reduced
@@ -238,14 +252,18 @@ __device__ __forceinline__ bool parse_record_global(const uint8_t* __restrict__ 
   return ok;
 }
 
-constexpr int kDecPad = 8;  // LDS bytes before / after each wave's window
+constexpr int kDecPad = 16;  // LDS bytes before / after each wave's window
 constexpr int kDecWindow = 64 * kMaxRecord + 8;
 
+// W16: the input is 16-B aligned, so the window is staged with 16-B loads and
+// LDS stores from the 16-B boundary at or below its start (else 4-B ones).
+template <bool W16>
 __global__ void __launch_bounds__(kCodecBlock) decode_kernel(const uint8_t* __restrict__ in, uint64_t in_bytes,
                                                              const uint64_t* __restrict__ offsets, uint64_t n,
                                                              uint8_t* __restrict__ vec, uint64_t* __restrict__ xs,
                                                              uint32_t* __restrict__ bad) {
-  __shared__ uint32_t s_win[kCodecBlock / 64][(kDecWindow + 2 * kDecPad) / 4];
+  constexpr int kRowWords = ((kDecWindow + 16 + 2 * kDecPad) / 4 + 3) & ~3;  // 16-B aligned rows
+  __shared__ __attribute__((aligned(16))) uint32_t s_win[kCodecBlock / 64][kRowWords];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint64_t e0 = (static_cast<uint64_t>(blockIdx.x) * kCodecBlock) + (threadIdx.x & ~63u);
   if (e0 >= n) return;  // wave-uniform
@@ -253,18 +271,28 @@ __global__ void __launch_bounds__(kCodecBlock) decode_kernel(const uint8_t* __re
   const bool valid = e < n;
   const uint64_t eN = e0 + 64 < n ? e0 + 64 : n;
   const uint64_t A = offsets[e0], Bend = offsets[eN];
-  const uint64_t A4 = A & ~3ull;
+  const uint64_t A4 = W16 ? (A & ~15ull) : (A & ~3ull);  // window base (all positions below are from it)
   uint64_t x = 0;
   uint32_t v[kLimbs];
   bool ok;
-  if (Bend >= A && Bend <= in_bytes && Bend - A4 <= static_cast<uint64_t>(kDecWindow)) {
+  if (Bend >= A && Bend <= in_bytes && Bend - A4 <= static_cast<uint64_t>(kDecWindow) + 12u) {
     uint32_t* S = s_win[wv] + kDecPad / 4;  // S[k] = dword at window byte 4k
     uint8_t* sb = reinterpret_cast<uint8_t*>(S);
-    const uint64_t B4 = Bend & ~3ull;
-    const uint32_t nw = static_cast<uint32_t>((B4 - A4) / 4);
-    const uint32_t* inw = reinterpret_cast<const uint32_t*>(in + A4);
-    for (uint32_t q = lane; q < nw; q += 64) S[q] = __builtin_nontemporal_load(inw + q);
-    if (lane < Bend - B4) sb[B4 - A4 + lane] = in[B4 + lane];
+    if constexpr (W16) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const uint64_t B16 = Bend & ~15ull;
+      const uint32_t nq = static_cast<uint32_t>((B16 - A4) / 16);
+      const u32x4* inq = reinterpret_cast<const u32x4*>(in + A4);
+      u32x4* Sq = reinterpret_cast<u32x4*>(S);
+      for (uint32_t q = lane; q < nq; q += 64) Sq[q] = __builtin_nontemporal_load(inq + q);
+      if (lane < Bend - B16) sb[B16 - A4 + lane] = in[B16 + lane];
+    } else {
+      const uint64_t B4 = Bend & ~3ull;
+      const uint32_t nw = static_cast<uint32_t>((B4 - A4) / 4);
+      const uint32_t* inw = reinterpret_cast<const uint32_t*>(in + A4);
+      for (uint32_t q = lane; q < nw; q += 64) S[q] = __builtin_nontemporal_load(inw + q);
+      if (lane < Bend - B4) sb[B4 - A4 + lane] = in[B4 + lane];
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -360,8 +388,16 @@ extern "C" int dn_m521_encode_shares(const void* vec, uint64_t n_elem, uint64_t 
                      xb.len, local, tot);
   hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, s, tot, nb, total);
   const uint64_t blocks = (n_elem + kCodecBlock - 1) / kCodecBlock;
-  hipLaunchKernelGGL(encode_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0, s, v, n_elem, xb,
-                     local, tot, offsets, out);
+  bool w16 = (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
+#ifdef DN_TUNING
+  if (tune_env("DN_ENCODE_W4") && tune_env("DN_ENCODE_W4")[0] == '1') w16 = false;  // A/B: 4-B stores
+#endif
+  if (w16)
+    hipLaunchKernelGGL(encode_kernel<true>, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0, s, v, n_elem,
+                       xb, local, tot, offsets, out);
+  else
+    hipLaunchKernelGGL(encode_kernel<false>, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0, s, v, n_elem,
+                       xb, local, tot, offsets, out);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_m521_encode_shares: %s", hipGetErrorString(err));
   return DN_OK;
@@ -372,9 +408,18 @@ extern "C" int dn_m521_decode_shares(const uint8_t* in, uint64_t in_bytes, const
   if (n_elem == 0) return DN_OK;
   if (!in || !offsets || !vec || !bad_count) return set_error(DN_ERR_ARG, "dn_m521_decode_shares: null pointer");
   const uint64_t blocks = (n_elem + kCodecBlock - 1) / kCodecBlock;
-  hipLaunchKernelGGL(decode_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0,
-                     static_cast<hipStream_t>(stream), in, in_bytes, offsets, n_elem, static_cast<uint8_t*>(vec), xs,
-                     bad_count);
+  bool w16 = (reinterpret_cast<uintptr_t>(in) & 15u) == 0;
+#ifdef DN_TUNING
+  if (tune_env("DN_DECODE_W4") && tune_env("DN_DECODE_W4")[0] == '1') w16 = false;  // A/B: 4-B staging
+#endif
+  if (w16)
+    hipLaunchKernelGGL(decode_kernel<true>, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0,
+                       static_cast<hipStream_t>(stream), in, in_bytes, offsets, n_elem, static_cast<uint8_t*>(vec), xs,
+                       bad_count);
+  else
+    hipLaunchKernelGGL(decode_kernel<false>, dim3(static_cast<uint32_t>(blocks)), dim3(kCodecBlock), 0,
+                       static_cast<hipStream_t>(stream), in, in_bytes, offsets, n_elem, static_cast<uint8_t*>(vec), xs,
+                       bad_count);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_m521_decode_shares: %s", hipGetErrorString(err));
   return DN_OK;

@@ -15,6 +15,8 @@ out = {}
 for r in os.environ.get("ROWS", "byte_api,draw_split").split(","):
     if r == "byte_api":
         out[r] = bench.byte_api_row()
+    elif r == "rows":  # every row of bench.py's rows_bench (mask, codec, envelope, PRNG split, sum, MiMC7)
+        out[r] = bench.rows_bench(dev, int(os.environ.get("LOG2N", "24")))
     elif r == "mask":
         out[r] = bench.mask_row(dev, int(os.environ.get("LOG2N", "24")))
     elif r == "draw_split":
