@@ -123,3 +123,40 @@ def test_decode_wide_windows_and_untrusted_offsets():
     far[-1] = far[-1] + (1 << 40)  # last record claims bytes far past the input
     with pytest.raises(ValueError):
         codec.decode_share_vec(packed, far, len(recs))
+
+
+@pytest.mark.parametrize("shift", [4, 8, 12])
+def test_unaligned_buffers_take_the_narrow_path(shift):
+    """Buffers not 16-B aligned (a 4-B-aligned slice of a larger allocation)
+    take the 4-B staging / store path of the codec kernels; results equal the
+    aligned (16-B) path byte for byte."""
+    import ctypes
+
+    L = codec._lib()
+    N = 5000 + shift
+    vals = [random.Random(shift * 100003 + i).randrange(P) for i in range(N)]
+    vec = torch.from_numpy(field.ints_to_vec(vals)).to(dev())
+    want_packed, want_offs = codec.encode_share_vec(vec, N, 3)
+    cap = int(L.dn_m521_encoded_capacity(N, 3))
+    big = torch.zeros(cap + 64, dtype=torch.uint8, device=dev())
+    out = big[shift:]  # data_ptr % 16 == shift
+    assert out.data_ptr() % 16 == shift
+    offs = torch.empty(N + 1, dtype=torch.int64, device=dev())
+    sb = int(L.dn_m521_codec_scratch_bytes(N))
+    scratch = torch.empty(sb, dtype=torch.uint8, device=dev())
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert L.dn_m521_encode_shares(vec.data_ptr(), N, 3, offs.data_ptr(), out.data_ptr(), cap, scratch.data_ptr(), sb,
+                                   st) == 0
+    total = int(want_offs[N].item())
+    assert torch.equal(offs, want_offs)
+    assert torch.equal(out[:total], want_packed)
+    # decode from the unaligned copy
+    back = torch.empty(field.vec_bytes(N), dtype=torch.uint8, device=dev())
+    xs = torch.empty(N, dtype=torch.int64, device=dev())
+    bad = torch.zeros(1, dtype=torch.int32, device=dev())
+    assert L.dn_m521_decode_shares(out.data_ptr(), total, offs.data_ptr(), N, back.data_ptr(), xs.data_ptr(),
+                                   bad.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0
+    assert field.vec_to_ints(back.cpu().numpy(), N) == vals
+    assert torch.all(xs == 3)
