@@ -11,7 +11,7 @@ and its inverse on the coordinator (coord/horizontal/agg.py:381-404):
 (dead member, alive member) key, then `unfix_precision`.
 
 `masked_sum` computes base + sum_j sign_j * make_mask(seed_j) in one pass per
-8 generators (dn_bounded_i64_accumulate), bit-exact with numpy: any generator
+16 generators (dn_bounded_i64_accumulate), bit-exact with numpy: any generator
 whose raw draws hit a Lemire rejection (odds 2^-47 per element) is replayed
 with the exact per-segment raw offsets numpy's sequential loop implies.
 """
