@@ -124,7 +124,10 @@ def test_split_2e24_digest_and_roundtrip():
     N = d["N"]
     sec = torch.from_numpy(secrets_int64(d["secret_seed"], N)).to(dev())
     ss = shamir.SecretShare(3)
-    for xs in ([1, 2, 3], [1, 3, 5], [2, 4, 5], [5, 3, 4], [1, 2, 3, 4, 5]):
+    import itertools
+
+    subsets = [list(c) for k in (3, 4, 5) for c in itertools.combinations(range(1, 6), k)] + [[5, 3, 4], [4, 1, 2]]
+    for xs in subsets:  # every 3-, 4- and 5-subset (and two unsorted ones): all Lagrange weight forms
         res, over = ss.resolve_shares_vec([out[x - 1] for x in xs], xs, N, return_overflow=True)
         assert torch.equal(res, sec), xs
         assert int(over.item()) == 0
