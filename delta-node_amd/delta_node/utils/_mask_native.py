@@ -64,6 +64,8 @@ def entropy_words(seed: Union[int, bytes, Sequence[int]]) -> List[int]:
 
     if isinstance(seed, int):
         return int_words(seed)
+    if isinstance(seed, (bytes, bytearray)):  # one word per byte (every byte < 2^32)
+        return list(seed)
     words: List[int] = []
     for v in (list(seed) if isinstance(seed, (bytes, bytearray)) else seed):
         words.extend(int_words(int(v)))
