@@ -523,13 +523,15 @@ static bool recon_unroll() {
 
 template <int A, int INV>
 static void launch_recon_k(int k, dim3 g, hipStream_t s, const ReconArgs& a) {
-  if (A == 1 && recon_unroll()) {
-    switch (k) {
-      case 2: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 2>), g, dim3(kBlock), 0, s, a); return;
-      case 3: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 3>), g, dim3(kBlock), 0, s, a); return;
-      case 4: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 4>), g, dim3(kBlock), 0, s, a); return;
-      case 5: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 5>), g, dim3(kBlock), 0, s, a); return;
-      default: break;
+  if constexpr (A == 1) {  // the unrolled share counts exist for one-limb weights only
+    if (recon_unroll()) {
+      switch (k) {
+        case 2: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 2>), g, dim3(kBlock), 0, s, a); return;
+        case 3: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 3>), g, dim3(kBlock), 0, s, a); return;
+        case 4: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 4>), g, dim3(kBlock), 0, s, a); return;
+        case 5: hipLaunchKernelGGL((reconstruct_kernel<A, INV, 5>), g, dim3(kBlock), 0, s, a); return;
+        default: break;
+      }
     }
   }
   hipLaunchKernelGGL((reconstruct_kernel<A, INV, 0>), g, dim3(kBlock), 0, s, a);
