@@ -41,14 +41,8 @@ __device__ __forceinline__ uint32_t y_len(const uint32_t v[kLimbs]) {
   return len;
 }
 
-// Same, reading only as many limbs as needed from the top: limb 16 (the u16
-// plane) is non-zero with odds 1 - 2^-9 for a uniform residue, so the length
-// pass usually reads 2 of the 66 bytes.
-__device__ __forceinline__ uint32_t y_len_mem(const uint8_t* vec, uint64_t e) {
-  const uint8_t* tb = tile_base(vec, static_cast<uint32_t>(e / kTile));
-  const uint32_t w = static_cast<uint32_t>(e % kTile);
-  const uint32_t top = reinterpret_cast<const uint16_t*>(tb + kHiOffset)[w] & kTopMask;
-  if (top) return 64u + (32u - __builtin_clz(top) + 7u) / 8u;
+// y length of element w of a tile from limbs 15 .. 0 (the top limb was zero)
+__device__ __noinline__ uint32_t y_len_low(const uint8_t* tb, uint32_t w) {
   for (int i = 15; i >= 0; --i) {
     const uint32_t l = reinterpret_cast<const uint32_t*>(tb)[i * kTile + w];
     if (l) return 4u * i + (32u - __builtin_clz(l) + 7u) / 8u;
@@ -56,62 +50,122 @@ __device__ __forceinline__ uint32_t y_len_mem(const uint8_t* vec, uint64_t e) {
   return 0u;
 }
 
+// Per 1024-element block: record lengths of 4 consecutive elements per thread
+// (one 8-B load of their top-limb u16s: the only read unless a top limb is
+// zero, odds 2^-9), their in-block exclusive prefix (wave scans by shuffles,
+// then across the 4 waves) as one 16-B store per thread, and the block total.
 __global__ void __launch_bounds__(kCodecBlock) lengths_scan_kernel(const uint8_t* __restrict__ vec, uint64_t n,
                                                                     uint32_t xlen, uint32_t* __restrict__ local,
                                                                     uint64_t* __restrict__ block_tot) {
-  __shared__ uint32_t s_sum[kCodecBlock];
+  __shared__ uint32_t s_w[kCodecBlock / 64];
   const uint64_t b = blockIdx.x;
-  const uint32_t t = threadIdx.x;
-  uint32_t len[4], sum = 0;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint64_t e0 = b * kScanElems + t * 4;  // 4 consecutive elements, one tile (256 % 4 == 0)
+  uint32_t len[4] = {0u, 0u, 0u, 0u};
+  if (e0 < n) {
+    const uint8_t* tb = tile_base(vec, static_cast<uint32_t>(e0 / kTile));
+    const uint32_t w0 = static_cast<uint32_t>(e0 % kTile);
+    uint16_t top[4];
+    if (e0 + 4 <= n) {
+      const uint64_t q = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(tb + kHiOffset) + w0 / 4);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint64_t e = b * kScanElems + t * 4 + j;
-    len[j] = 0;
-    if (e < n) len[j] = 1u + xlen + y_len_mem(vec, e);
-    sum += len[j];
+      for (int j = 0; j < 4; ++j) top[j] = static_cast<uint16_t>(q >> (16 * j));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) top[j] = e0 + j < n ? reinterpret_cast<const uint16_t*>(tb + kHiOffset)[w0 + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (e0 + j < n) {
+        const uint32_t tp = top[j] & kTopMask;
+        len[j] = 1u + xlen + (tp ? 64u + (32u - __builtin_clz(tp) + 7u) / 8u : y_len_low(tb, w0 + j));
+      }
+    }
   }
-  s_sum[t] = sum;
+  const uint32_t sum = len[0] + len[1] + len[2] + len[3];
+  uint32_t inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(inc, d);
+    if (lane >= static_cast<uint32_t>(d)) inc += v;
+  }
+  if (lane == 63) s_w[wv] = inc;
   __syncthreads();
-  for (int off = 1; off < kCodecBlock; off <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t add = t >= static_cast<uint32_t>(off) ? s_sum[t - off] : 0u;
-    __syncthreads();
-    s_sum[t] += add;
-    __syncthreads();
-  }
-  uint32_t run = s_sum[t] - sum;  // exclusive prefix of this thread's 4 elements
+  uint32_t wbase = 0, tot = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint64_t e = b * kScanElems + t * 4 + j;
-    if (e < n) local[e] = run;
-    run += len[j];
+  for (int w = 0; w < kCodecBlock / 64; ++w) {
+    wbase += (w < static_cast<int>(wv)) ? s_w[w] : 0u;
+    tot += s_w[w];
   }
-  if (t == kCodecBlock - 1) block_tot[b] = s_sum[t];
+  uint32_t run = wbase + inc - sum;  // exclusive prefix of this thread's 4 elements
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 o;
+  o.x = run;
+  o.y = run + len[0];
+  o.z = run + len[0] + len[1];
+  o.w = run + len[0] + len[1] + len[2];
+  if (e0 + 4 <= n) {
+    __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(local + e0));
+  } else {
+    const uint32_t ov[4] = {o.x, o.y, o.z, o.w};
+    for (int j = 0; j < 4; ++j)
+      if (e0 + j < n) local[e0 + j] = ov[j];
+  }
+  if (t == 0) block_tot[b] = tot;
 }
 
-// Exclusive scan of the block totals in one workgroup (nb <= a few 10^5).
-__global__ void __launch_bounds__(1024) scan_blocks_kernel(uint64_t* __restrict__ tot, uint64_t nb,
-                                                           uint64_t* __restrict__ total_out) {
-  __shared__ uint64_t s[1024];
-  const uint32_t t = threadIdx.x;
-  const uint64_t per = (nb + 1023) / 1024;
-  const uint64_t lo = t * per, hi = lo + per < nb ? lo + per : nb;
-  uint64_t sum = 0;
-  for (uint64_t i = lo; i < hi; ++i) sum += tot[i];
-  s[t] = sum;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const uint64_t add = t >= static_cast<uint32_t>(off) ? s[t - off] : 0ull;
+// Exclusive scan of the block totals in one workgroup: the totals
+// are staged in LDS as 32-bit words (a block's total is at most 1024 * 76
+// bytes) with coalesced loads, each thread scans a contiguous run of them
+// (padded rows: no bank conflicts), the run sums are scanned across threads.
+constexpr int kScanThreads = 1024;
+constexpr int kScanStage = 8192;  // totals staged per pass (34 KB of LDS)
+
+__global__ void __launch_bounds__(kScanThreads) scan_blocks_kernel(uint64_t* __restrict__ tot, uint64_t nb,
+                                                                   uint64_t* __restrict__ total_out) {
+  __shared__ uint32_t s[kScanStage + kScanStage / 8];  // row of 8 + 1 pad per thread
+  __shared__ uint64_t s_w[kScanThreads / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  uint64_t carry = 0;  // total of the previous passes
+  for (uint64_t base = 0; base < nb; base += kScanStage) {
+    const uint32_t m = static_cast<uint32_t>(nb - base < kScanStage ? nb - base : kScanStage);
+    for (uint32_t i = t; i < m; i += kScanThreads) s[i + i / 8] = static_cast<uint32_t>(tot[base + i]);
     __syncthreads();
-    s[t] += add;
+    // thread t: totals 8 t .. 8 t + 7 of this pass
+    uint64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = 8u * t + j;
+      sum += i < m ? s[i + i / 8] : 0u;
+    }
+    uint64_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t v = __shfl_up(inc, d);
+      if (lane >= static_cast<uint32_t>(d)) inc += v;
+    }
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint64_t wbase = 0, ptot = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+      wbase += (w < static_cast<int>(wv)) ? s_w[w] : 0u;
+      ptot += s_w[w];
+    }
+    uint64_t run = carry + wbase + inc - sum;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = 8u * t + j;
+      if (i < m) {
+        const uint32_t v = s[i + i / 8];
+        tot[base + i] = run;
+        run += v;
+      }
+    }
+    carry += ptot;
     __syncthreads();
   }
-  uint64_t run = s[t] - sum;
-  for (uint64_t i = lo; i < hi; ++i) {
-    const uint64_t v = tot[i];
-    tot[i] = run;
-    run += v;
-  }
-  if (t == 1023) *total_out = s[1023];
+  if (t == 0) *total_out = carry;
 }
 
 // One wave = 64 consecutive elements = one contiguous run of records.
