@@ -9,8 +9,9 @@
 // keyed by the previous step's result, each hash is 13 rounds of t^7 (4
 // dependent field products), so a weight costs 52 strictly dependent 254-bit
 // Montgomery products and nothing can run beside them.  A GPU lane runs such a
-// chain at its dependent-instruction latency (~1.2 us per product on one
-// gfx950 lane, measured: 67.7 us per weight); a host core with 64x64->128-bit
+// chain at its dependent-instruction latency (measured on one gfx950 lane:
+// 67.7 us per weight with 8x32-bit CIOS, 33 us with the 29-bit separated-operand
+// product of mimc7_bn254.hip); a host core with 64x64->128-bit
 // multiplies does a 4-limb CIOS product in tens of ns.  The parallel parts of
 // the row (calc_data_commitment's row hashes and Merkle blocks) stay on the
 // GPU (mimc7_bn254.hip).  The weights are host data in the reference's caller

@@ -10,9 +10,18 @@
 //   rows padded to a multiple of 128, hash_arr(row, 2) per row, then a
 //   binary Merkle tree of hash_arr([left, right], 2) per 128-row block.
 //
-// Arithmetic: Montgomery (R = 2^256, CIOS, 8 x 32-bit limbs, one element per
-// lane); everything stays in Montgomery form between rounds (sums commute
-// with the form).  t^7 = ((t^2 t)^2) t: 4 products per round.  The row pass
+// Arithmetic: Montgomery over 9 x 29-bit limbs (R = 2^261, one element per
+// lane), separated operand scanning: the 81 limb products of a b and the 81 of
+// m q go into 64-bit column accumulators (29-bit limbs leave room for 18
+// products per column), so every v_mad_u64_u32 takes its addend straight from
+// the accumulator pair — no carry chain per product, no register moves to
+// build zero-extended addends (the 8 x 32-bit CIOS form compiled to ~750 VALU
+// per product, this one to ~250) and short dependency chains.  R > 170 q, so
+// products of operands below 3 q still leave a result below 2 q: the round
+// sums r + k + c are carry-normalized but not reduced.  Everything stays in
+// Montgomery form between rounds (sums commute with the form);
+// t^7 = ((t^2 t)^2) t: 4 products per round.  Field values cross memory as
+// 8 x 32-bit plain limbs.  The row pass
 // is one lane per row (rows are independent chains); the Merkle pass is one
 // 64-lane workgroup per 128-leaf block, levels handed over through LDS.
 // The weight commitment is one sequential chain by definition (each step
@@ -30,13 +39,16 @@ namespace mimc {
 
 constexpr int L = 8;
 
+constexpr int N = 9;                 // 29-bit limbs of the Montgomery form
+constexpr uint32_t kM29 = (1u << 29) - 1;
+
 struct Consts {
-  uint32_t q[L];
-  uint32_t qinv;          // -q^{-1} mod 2^32
-  uint32_t r2[L];         // R^2 mod q
-  uint32_t one[L];        // R mod q (1 in Montgomery form)
-  uint32_t half_q[L];     // floor(q / 2)
-  uint32_t cts[kRounds][L];  // round constants, Montgomery form
+  uint32_t q[L];             // 32-bit limbs (float_to_field)
+  uint32_t half_q[L];        // floor(q / 2), 32-bit limbs
+  uint32_t q29[N];           // q, 29-bit limbs
+  uint32_t qinv;             // -q^{-1} mod 2^29
+  uint32_t r2[N];            // R^2 mod q, R = 2^261
+  uint32_t cts[kRounds][N];  // round constants, Montgomery form
 };
 
 // ---- 256-bit helpers (host + device) ----
@@ -73,70 +85,130 @@ __host__ __device__ inline void addmod(uint32_t a[L], const uint32_t b[L], const
   if (geq(a, q)) sub_in(a, q);
 }
 
-// CIOS Montgomery product: r = a b R^{-1} mod q (inputs < q, output < q).
-__host__ __device__ inline void mont_mul(uint32_t r[L], const uint32_t a[L], const uint32_t b[L], const Consts& k) {
-  uint32_t t[L + 2];
-  for (int i = 0; i < L + 2; ++i) t[i] = 0;
-#pragma unroll
-  for (int i = 0; i < L; ++i) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      const uint64_t s = static_cast<uint64_t>(a[j]) * b[i] + t[j] + c;
-      t[j] = static_cast<uint32_t>(s);
-      c = s >> 32;
-    }
-    uint64_t s = static_cast<uint64_t>(t[L]) + c;
-    t[L] = static_cast<uint32_t>(s);
-    t[L + 1] = static_cast<uint32_t>(s >> 32);
-    const uint32_t m = t[0] * k.qinv;
-    c = (static_cast<uint64_t>(m) * k.q[0] + t[0]) >> 32;
-#pragma unroll
-    for (int j = 1; j < L; ++j) {
-      const uint64_t s2 = static_cast<uint64_t>(m) * k.q[j] + t[j] + c;
-      t[j - 1] = static_cast<uint32_t>(s2);
-      c = s2 >> 32;
-    }
-    s = static_cast<uint64_t>(t[L]) + c;
-    t[L - 1] = static_cast<uint32_t>(s);
-    t[L] = t[L + 1] + static_cast<uint32_t>(s >> 32);
+// ---- 29-bit limb form (host + device) ----
+__host__ __device__ inline void to29(const uint32_t a[L], uint32_t o[N]) {
+  for (int i = 0; i < N; ++i) {
+    const int bit = 29 * i, w = bit / 32, sh = bit % 32;
+    const uint64_t lo = a[w], hi = w + 1 < L ? a[w + 1] : 0u;
+    o[i] = static_cast<uint32_t>(((hi << 32) | lo) >> sh) & kM29;
   }
-  for (int i = 0; i < L; ++i) r[i] = t[i];
-  if (t[L] || geq(r, k.q)) sub_in(r, k.q);
 }
 
-__host__ __device__ inline void to_mont(uint32_t r[L], const uint32_t a[L], const Consts& k) { mont_mul(r, a, k.r2, k); }
+__host__ __device__ inline void from29(const uint32_t o[N], uint32_t a[L]) {
+  uint64_t acc = 0;
+  int nb = 0, w = 0;
+  for (int i = 0; i < N; ++i) {
+    acc |= static_cast<uint64_t>(o[i]) << nb;
+    nb += 29;
+    while (nb >= 32 && w < L) {
+      a[w++] = static_cast<uint32_t>(acc);
+      acc >>= 32;
+      nb -= 32;
+    }
+  }
+  while (w < L) {
+    a[w++] = static_cast<uint32_t>(acc);
+    acc >>= 32;
+  }
+}
 
-__host__ __device__ inline void from_mont(uint32_t r[L], const uint32_t a[L], const Consts& k) {
-  uint32_t one[L] = {1, 0, 0, 0, 0, 0, 0, 0};
-  mont_mul(r, a, one, k);
+__host__ __device__ inline bool geq29(const uint32_t a[N], const uint32_t b[N]) {
+  for (int i = N - 1; i >= 0; --i)
+    if (a[i] != b[i]) return a[i] > b[i];
+  return true;
+}
+
+__host__ __device__ inline void sub29_in(uint32_t a[N], const uint32_t b[N]) {  // a -= b (a >= b)
+  uint32_t br = 0;
+  for (int i = 0; i < N; ++i) {
+    const uint32_t d = a[i] - b[i] - br;  // in (-2^30, 2^29)
+    br = d >> 31;
+    a[i] = d & kM29;
+  }
+}
+
+// carries of limbs up to 2^32 - 1 into their neighbours (the value fits 9 limbs)
+__host__ __device__ inline void norm29(uint32_t a[N]) {
+  uint32_t c = 0;
+  for (int i = 0; i < N; ++i) {
+    const uint32_t v = a[i] + c;
+    a[i] = v & kM29;
+    c = v >> 29;
+  }
+}
+
+// a = (a + b) mod q for a, b < q
+__host__ __device__ inline void addmod29(uint32_t a[N], const uint32_t b[N], const uint32_t q[N]) {
+  for (int i = 0; i < N; ++i) a[i] += b[i];
+  norm29(a);
+  if (geq29(a, q)) sub29_in(a, q);
+}
+
+// Montgomery product r = a b R^{-1} mod q for a, b < 3 q (normalized limbs),
+// r < q.  Columns T[i + j] accumulate a_i b_j and m_i q_j (at most 18 products
+// of < 2^58 plus a carry < 2^35: below 2^63).
+__host__ __device__ inline void mont_mul(uint32_t r[N], const uint32_t a[N], const uint32_t b[N], const Consts& k) {
+  uint64_t T[2 * N];
+#pragma unroll
+  for (int i = 0; i < 2 * N; ++i) T[i] = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) T[i + j] += static_cast<uint64_t>(a[i]) * b[j];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t m = (static_cast<uint32_t>(T[i]) * k.qinv) & kM29;
+#pragma unroll
+    for (int j = 0; j < N; ++j) T[i + j] += static_cast<uint64_t>(m) * k.q29[j];
+    T[i + 1] += T[i] >> 29;  // the low 29 bits of T[i] are now zero
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t v = T[N + i] + c;
+    r[i] = static_cast<uint32_t>(v) & kM29;
+    c = v >> 29;
+  }
+  if (geq29(r, k.q29)) sub29_in(r, k.q29);
+}
+
+// plain 32-bit limbs (< q) -> Montgomery form, and back (canonical)
+__host__ __device__ inline void to_mont(uint32_t r[N], const uint32_t a[L], const Consts& k) {
+  uint32_t a29[N];
+  to29(a, a29);
+  mont_mul(r, a29, k.r2, k);
+}
+
+__host__ __device__ inline void from_mont(uint32_t r[L], const uint32_t a[N], const Consts& k) {
+  uint32_t one[N] = {1, 0, 0, 0, 0, 0, 0, 0, 0}, t[N];
+  mont_mul(t, a, one, k);
+  from29(t, r);
 }
 
 // mimc7_hash in Montgomery form: (r_13 + k) mod q in `out` (Montgomery).
-__host__ __device__ inline void hash_m(uint32_t out[L], const uint32_t x[L], const uint32_t key[L], const Consts& k) {
-  uint32_t r[L];
-  for (int i = 0; i < L; ++i) r[i] = x[i];
+__host__ __device__ inline void hash_m(uint32_t out[N], const uint32_t x[N], const uint32_t key[N], const Consts& k) {
+  uint32_t r[N];
+  for (int i = 0; i < N; ++i) r[i] = x[i];
   for (int c = 0; c < kRounds; ++c) {
-    uint32_t t[L];
-    for (int i = 0; i < L; ++i) t[i] = r[i];
-    addmod(t, key, k.q);
-    addmod(t, k.cts[c], k.q);
-    uint32_t t2[L], t3[L], t6[L];
+    uint32_t t[N];
+    for (int i = 0; i < N; ++i) t[i] = r[i] + key[i] + k.cts[c][i];  // < 3 q: not reduced
+    norm29(t);
+    uint32_t t2[N], t3[N], t6[N];
     mont_mul(t2, t, t, k);
     mont_mul(t3, t2, t, k);
     mont_mul(t6, t3, t3, k);
     mont_mul(r, t6, t, k);
   }
-  for (int i = 0; i < L; ++i) out[i] = r[i];
-  addmod(out, key, k.q);
+  for (int i = 0; i < N; ++i) out[i] = r[i];
+  addmod29(out, key, k.q29);
 }
 
 // One chain step of mimc7_hash_arr: r <- (r + x + mimc7_hash(x, r)) mod q.
-__host__ __device__ inline void arr_step(uint32_t r[L], const uint32_t x[L], const Consts& k) {
-  uint32_t h[L];
+__host__ __device__ inline void arr_step(uint32_t r[N], const uint32_t x[N], const Consts& k) {
+  uint32_t h[N];
   hash_m(h, x, r, k);
-  addmod(r, x, k.q);
-  addmod(r, h, k.q);
+  addmod29(r, x, k.q29);
+  addmod29(r, h, k.q29);
 }
 
 // _float2mpz: field value (plain, < q) of min(a, q - a), a = int(v * 10^p);
@@ -194,14 +266,14 @@ struct RowArgs {
 __global__ void __launch_bounds__(256) rows_kernel(const RowArgs a) {
   const uint64_t row = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (row >= a.rows_pad) return;
-  uint32_t r[L];
+  uint32_t r[N];
   {  // key 2 in Montgomery form
-    uint32_t two[L] = {2, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t two[L] = {2, 0, 0, 0, 0, 0, 0, 0};
     to_mont(r, two, a.k);
   }
   bool ok = true;
   for (int c = 0; c < a.cols; ++c) {
-    uint32_t x[L], xm[L];
+    uint32_t x[L], xm[N];
     if (row < a.rows) {
       const double v = a.data[row * a.cols + c];
       ok &= float_to_field(v, c == a.cols - 1 ? a.scale_label : a.scale_feat, x, a.k);
@@ -225,37 +297,37 @@ struct MerkleArgs {
 
 // One workgroup of 64 lanes per 128-leaf block: level sizes 64, 32, ..., 1.
 __global__ void __launch_bounds__(64) merkle_kernel(const MerkleArgs a) {
-  __shared__ uint32_t s[64][L];
+  __shared__ uint32_t s[64][N];
   const uint32_t t = threadIdx.x;
   const uint32_t* lv = a.leaves + static_cast<uint64_t>(blockIdx.x) * 128 * L;
-  uint32_t key[L];
+  uint32_t key[N];
   {
-    uint32_t two[L] = {2, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t two[L] = {2, 0, 0, 0, 0, 0, 0, 0};
     to_mont(key, two, a.k);
   }
-  uint32_t l[L], r[L], lm[L], rm[L], acc[L];
+  uint32_t l[L], r[L], lm[N], rm[N], acc[N];
   for (int i = 0; i < L; ++i) {
     l[i] = lv[(2 * t) * L + i];
     r[i] = lv[(2 * t + 1) * L + i];
   }
   to_mont(lm, l, a.k);
   to_mont(rm, r, a.k);
-  for (int i = 0; i < L; ++i) acc[i] = key[i];
+  for (int i = 0; i < N; ++i) acc[i] = key[i];
   arr_step(acc, lm, a.k);
   arr_step(acc, rm, a.k);
-  for (int i = 0; i < L; ++i) s[t][i] = acc[i];  // Montgomery form from here on
+  for (int i = 0; i < N; ++i) s[t][i] = acc[i];  // Montgomery form from here on
   __syncthreads();
   for (uint32_t width = 32; width >= 1; width >>= 1) {
-    uint32_t nxt[L];
+    uint32_t nxt[N];
     const bool act = t < width;
     if (act) {
-      for (int i = 0; i < L; ++i) nxt[i] = key[i];
+      for (int i = 0; i < N; ++i) nxt[i] = key[i];
       arr_step(nxt, s[2 * t], a.k);
       arr_step(nxt, s[2 * t + 1], a.k);
     }
     __syncthreads();
     if (act)
-      for (int i = 0; i < L; ++i) s[t][i] = nxt[i];
+      for (int i = 0; i < N; ++i) s[t][i] = nxt[i];
     __syncthreads();
   }
   if (t == 0) {
@@ -277,11 +349,11 @@ struct ChainArgs {
 
 __global__ void chain_kernel(const ChainArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t r[L];
+  uint32_t r[N];
   to_mont(r, a.key, a.k);
   bool ok = true;
   for (uint64_t i = 0; i < a.n; ++i) {
-    uint32_t x[L], xm[L];
+    uint32_t x[L], xm[N];
     ok &= float_to_field(a.w[i], a.scale, x, a.k);
     to_mont(xm, x, a.k);
     arr_step(r, xm, a.k);
@@ -303,21 +375,20 @@ struct HashArgs {
 __global__ void __launch_bounds__(256) hash_kernel(const HashArgs a) {
   const uint64_t e = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (e >= a.n) return;
-  uint32_t x[L], k[L], xm[L], km[L];
+  uint32_t x[L], k[L], xm[N], km[N];
   for (int i = 0; i < L; ++i) {
     x[i] = a.x[e * L + i];
     k[i] = a.key[e * L + i];
   }
   to_mont(xm, x, a.k);
   to_mont(km, k, a.k);
-  uint32_t r[L];
-  for (int i = 0; i < L; ++i) r[i] = xm[i];
+  uint32_t r[N];
+  for (int i = 0; i < N; ++i) r[i] = xm[i];
   for (int c = 0; c < kRounds; ++c) {
-    uint32_t t[L];
-    for (int i = 0; i < L; ++i) t[i] = r[i];
-    addmod(t, km, a.k.q);
-    addmod(t, a.k.cts[c], a.k.q);
-    uint32_t t2[L], t3[L], t6[L];
+    uint32_t t[N];
+    for (int i = 0; i < N; ++i) t[i] = r[i] + km[i] + a.k.cts[c][i];  // < 3 q
+    norm29(t);
+    uint32_t t2[N], t3[N], t6[N];
     mont_mul(t2, t, t, a.k);
     mont_mul(t3, t2, t, a.k);
     mont_mul(t6, t3, t3, a.k);
@@ -334,19 +405,19 @@ __global__ void __launch_bounds__(256) hash_kernel(const HashArgs a) {
 void make_consts(Consts& k) {
   const uint32_t* q = kQ32;
   std::memcpy(k.q, q, sizeof(k.q));
-  // qinv = -q^{-1} mod 2^32 (Newton)
+  to29(q, k.q29);
+  // qinv = -q^{-1} mod 2^29 (Newton mod 2^32, then the low 29 bits)
   uint32_t inv = q[0];
   for (int i = 0; i < 5; ++i) inv *= 2u - q[0] * inv;
-  k.qinv = 0u - inv;
-  // R mod q and R^2 mod q by doubling 1 (mod q) 256 / 512 times
+  k.qinv = (0u - inv) & kM29;
+  // R^2 mod q, R = 2^261: double 1 (mod q) 522 times
   uint32_t v[L] = {1, 0, 0, 0, 0, 0, 0, 0};
-  for (int it = 1; it <= 512; ++it) {
+  for (int it = 0; it < 2 * 29 * N; ++it) {
     uint32_t t[L];
     std::memcpy(t, v, sizeof(t));
     addmod(v, t, q);
-    if (it == 256) std::memcpy(k.one, v, sizeof(v));
   }
-  std::memcpy(k.r2, v, sizeof(v));
+  to29(v, k.r2);
   // floor(q / 2)
   for (int i = 0; i < L; ++i) k.half_q[i] = (q[i] >> 1) | (i + 1 < L ? (q[i + 1] << 31) : 0u);
 }
