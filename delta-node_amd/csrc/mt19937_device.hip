@@ -112,16 +112,28 @@ __device__ __forceinline__ uint32_t append64(uint32_t (&Q)[11], const Lanes& L) 
 }
 
 // Jump table of one source window W, E[v] = words 0..683 of the stream of
-// T[v] = sum over bits j of v of f^j(W), stored for b128 reads: entry (v, m)
-// is a 28-word row holding E[v][64 k + m - 16] for k = 0..10 (words 0..10)
-// and again for k = 1..10 (words 12..21), zero outside 0..683, so the ten
-// words a lane XORs into its ten window registers for one chunk are one
-// 16-B-aligned run of a row (two ds_read_b128 + one ds_read_b64).  The 28-word
-// pitch spreads a b128 lane group over all 64 banks (a 24-word pitch reads
-// every group 2-way conflicted: 356 vs 252 LDS cycles per 16 chunks).
-constexpr int kEPitch = 28;
-constexpr int kEVWords = 64 * kEPitch;  // words per chunk value v
-constexpr int kJumpWaves = 8;           // jumps (waves) per workgroup, all from one source
+// T[v] = sum over bits j of v of f^j(W), laid out for ds_read_b64.  The ten
+// words a lane XORs into its window registers for one chunk are E[v][64 k +
+// m - 16] for k = 0..9 (main half) or k = 1..10 (wrap half, lanes whose row
+// index wraps); they are stored as five 8-B pairs, pair i of (v, m) at
+//   half * kEWrap + i * kEPair + (64 v + m) * 2
+// so one chunk is five ds_read_b64 at immediate offsets from one address.
+// Banking (64 x 4-B banks, a b64 lane group = 32 lanes = 64 banks): a lane
+// group reads 32 consecutive rows m (mod 64) of one pair plane -> 32
+// distinct bank pairs, and kEWrap is a multiple of 64 words, so wrapped lanes
+// keep their pairs: conflict-free (SQ_LDS_BANK_CONFLICT ~0), 160 LDS cycles
+// per 16 chunks.  kEPair is 8 B off a multiple of 512 B so the compiler cannot
+// fuse the five reads into ds_read2(st64)_b64 (half-rate, banks mod 32).
+// A/B at 2^24 (profiles/r02/mt_jump_layout.md): the earlier 28-word rows
+// (two b128 + one b64, wrap copy at +12 words) took 252 cycles by the bank
+// model, SQ_LDS_BANK_CONFLICT +54 % of the array cycles, and the level of
+// 2016 jumps 0.37-0.41 ms; this layout 0.29-0.31 ms; 12-word rows read as
+// three b128 (conflict-free by the model, 192 cycles) 0.34-0.37 ms.
+constexpr int kEVWords = 64 * 2;                      // words per chunk value v in one pair plane
+constexpr int kEPair = 16 * kEVWords + 2;              // 2050 words
+constexpr int kEWrap = ((5 * kEPair + 63) / 64) * 64;  // 10304 words
+constexpr int kEWords = kEWrap + 5 * kEPair;           // 82 KB
+constexpr int kJumpWaves = 8;  // jumps (waves) per workgroup, all from one source
 
 // a ^ b ^ c in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96;
 // hipcc keeps two v_xor_b32 otherwise)
@@ -134,11 +146,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // the ten table words of chunk t (value c) for this lane: off = the lane's row offset for t
 __device__ __forceinline__ void table_words(const uint32_t* E, uint32_t off, uint32_t c, uint32_t (&x)[10]) {
   const uint32_t* p = E + c * kEVWords + off;
-  const u32x4_t a = *reinterpret_cast<const u32x4_t*>(p);
-  const u32x4_t b = *reinterpret_cast<const u32x4_t*>(p + 4);
-  const u32x2_t d = *reinterpret_cast<const u32x2_t*>(p + 8);
-  x[0] = a.x, x[1] = a.y, x[2] = a.z, x[3] = a.w, x[4] = b.x, x[5] = b.y, x[6] = b.z, x[7] = b.w, x[8] = d.x,
-  x[9] = d.y;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const u32x2_t d = *reinterpret_cast<const u32x2_t*>(p + i * kEPair);
+    x[2 * i] = d.x, x[2 * i + 1] = d.y;
+  }
 }
 
 // One Horner step over the 64-bit word gw of g in frame K (logical register
@@ -182,13 +194,13 @@ __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, cons
 // groups them; padding jobs have dst < 0).  Horner over 4-bit chunks of g,
 // 16 chunks (one 64-bit word of g) per step: r <- f^64(r) ^ sum_t
 // f^(4 (15 - t))(T[c_t]); f^m(T[v]) is the window at offset m of T[v]'s own
-// stream, which the workgroup tables once (E, 96 KB of LDS), so a step is
+// stream, which the workgroup tables once (E, 82 KB of LDS), so a step is
 //   * f^64(r): 64 new words mix(r[l], r[l+1], r[l+397]), l = 0..63 — one
 //     register, its operands gathered by 3 ds_bpermute;
 //   * the XOR of 16 table windows into the 624 window words (10 registers;
-//     48 LDS reads and 80 v_bitop3 per lane).
+//     80 ds_read_b64 and 80 v_bitop3 per lane).
 __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t E[16 * kEVWords];
+  __shared__ __attribute__((aligned(16))) uint32_t E[kEWords];
   __shared__ uint32_t ext[kMtN + 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint32_t j0 = blockIdx.x * kJumpWaves;
@@ -200,12 +212,14 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
   __syncthreads();
   if (tid < 63u) ext[kMtN + tid] = mt_mix(ext[tid], ext[tid + 1], ext[tid + kMtM]);
   __syncthreads();
-  for (uint32_t e = tid; e < 16u * kEVWords; e += 64u * kJumpWaves) {
-    const uint32_t v = e / kEVWords, rem = e - v * kEVWords, m = rem / kEPitch, k = rem - m * kEPitch;
-    const int kk = k < 11u ? static_cast<int>(k) : (k >= 12u && k < 22u ? static_cast<int>(k) - 11 : -1);
-    const int j = 64 * kk + static_cast<int>(m) - 16;  // T-stream word
+  for (uint32_t e = tid; e < static_cast<uint32_t>(kEWords); e += 64u * kJumpWaves) {
+    const uint32_t wrap = e >= static_cast<uint32_t>(kEWrap) ? 1u : 0u, re = e - wrap * kEWrap;
+    const uint32_t i = re / kEPair, rem = re - i * kEPair;  // pair plane, position in it
+    const uint32_t v = rem / kEVWords, mw = rem - v * kEVWords, m = mw >> 1;
+    // T-stream word; -1 in the gap before the wrap half and the 2 pad words of a plane
+    const int j = (i < 5u && v < 16u) ? 64 * static_cast<int>(2 * i + (mw & 1u) + wrap) + static_cast<int>(m) - 16 : -1;
     uint32_t x = 0u;
-    if (kk >= 0 && j >= 0 && j < 684) {
+    if (j >= 0 && j < 684) {
 #pragma unroll
       for (int b = 0; b < 4; ++b) x ^= ext[j + b] & (0u - ((v >> b) & 1u));
     }
@@ -228,7 +242,7 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
     const uint32_t u = lane + 60u - 4u * t;
-    off[t] = (u & 63u) * kEPitch + (u >> 6) * 12u;
+    off[t] = (u & 63u) * 2u + (u >> 6) * static_cast<uint32_t>(kEWrap);
   }
   int top = kMtPolyWords - 1;
   while (top > 0 && g[top] == 0ull) --top;  // steps above it leave r = 0
