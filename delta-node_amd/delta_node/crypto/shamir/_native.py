@@ -10,6 +10,7 @@ loaded (same soname), i.e. one runtime, one set of streams per process.
 """
 from __future__ import annotations
 
+import array
 import contextlib
 import ctypes
 import os
@@ -275,24 +276,29 @@ def mt_draw_coeffs(rng, n: int, tm1: int) -> np.ndarray:
     out = np.zeros(max(tm1, 0) * vb, dtype=np.uint8)
     if tm1 <= 0 or n == 0:
         return out.reshape(max(tm1, 0), vb)
-    version, internal, gauss = rng.getstate()
-    state = (ctypes.c_uint32 * 624)(*internal[:624])
-    index = ctypes.c_int32(internal[624])
+    version, gauss, state, index = _mt_state(rng)
     check(lib().dn_mt19937_draw_coeffs(state, ctypes.byref(index), n, tm1, out.ctypes.data))
-    rng.setstate((version, tuple(state) + (index.value,), gauss))
+    _mt_set_state(rng, version, gauss, state, index)
     return out.reshape(tm1, vb)
 
 
 def _mt_state(rng):
+    """rng's MT19937 array as a ctypes uint32[624] (over an array.array: ~10x
+    cheaper than building a ctypes array from 624 Python ints) and its index."""
     version, internal, gauss = rng.getstate()
-    return version, gauss, (ctypes.c_uint32 * 624)(*internal[:624]), ctypes.c_int32(internal[624])
+    buf = array.array("I", internal[:624])
+    return version, gauss, (ctypes.c_uint32 * 624).from_buffer(buf), ctypes.c_int32(internal[624])
+
+
+def _mt_set_state(rng, version, gauss, state, index) -> None:
+    rng.setstate((version, tuple(memoryview(state).cast("B").cast("I").tolist()) + (index.value,), gauss))
 
 
 def mt_skip(rng, words: int) -> None:
     """Advance `rng` (a random.Random) by `words` 32-bit outputs by jump-ahead."""
     version, gauss, state, index = _mt_state(rng)
     check(lib().dn_mt19937_skip(state, ctypes.byref(index), int(words)))
-    rng.setstate((version, tuple(state) + (index.value,), gauss))
+    _mt_set_state(rng, version, gauss, state, index)
 
 
 def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
@@ -317,7 +323,7 @@ def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
     if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
         return False
     check(rc)
-    rng.setstate((version, tuple(state) + (index.value,), gauss))
+    _mt_set_state(rng, version, gauss, state, index)
     return True
 
 
@@ -340,7 +346,7 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
     if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
         return False
     check(rc)
-    rng.setstate((version, tuple(state) + (index.value,), gauss))
+    _mt_set_state(rng, version, gauss, state, index)
     return True
 
 

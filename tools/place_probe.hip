@@ -9,6 +9,9 @@
 //            without its loads
 //   split5   the split's full access pattern (140 B read, 330 B written per
 //            element), arithmetic replaced by XORs
+//   write5il / split5il  the same with a tile-interleaved share block
+//            ([tile][share][plane]: each wave writes one contiguous 5-tile
+//            run instead of 5 runs vec_bytes apart)
 //
 // build: hipcc -O3 --offload-arch=gfx950 -I../delta-node_amd/csrc place_probe.hip -o place_probe
 #include <hip/hip_runtime.h>
@@ -61,7 +64,7 @@ __global__ void write1b(u32x4* __restrict__ out, size_t n) {
   }
 }
 
-template <bool READS>
+template <bool READS, bool IL = false>
 __global__ void __launch_bounds__(256) split5(const int64_t* __restrict__ sec, const uint8_t* __restrict__ co,
                                               uint8_t* __restrict__ sh, uint32_t ntiles, uint64_t vb, int nsh) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -88,7 +91,10 @@ __global__ void __launch_bounds__(256) split5(const int64_t* __restrict__ sec, c
         for (int i = 0; i < kLimbs; ++i) v[i] = c1[i] ^ c2[i] ^ (uint32_t)x;
         v[0] ^= (uint32_t)s;
         v[16] &= kTopMask;
-        store_fe(tile_base(sh + (uint64_t)x * vb, tile), w, v);
+        if constexpr (IL)
+          store_fe(tile_base(sh, tile * (uint32_t)nsh + (uint32_t)x), w, v);
+        else
+          store_fe(tile_base(sh + (uint64_t)x * vb, tile), w, v);
       }
     }
   }
@@ -278,11 +284,14 @@ int main(int argc, char** argv) {
       const float r1 = time_ms([&] { read1<<<4096, 256>>>((const u32x4*)p, n16, sink); }, reps);
       const float w5 = time_ms([&] { split5<false><<<256, 256>>>(sec, co, p, ntiles, vb, 5); }, reps);
       const float s5 = time_ms([&] { split5<true><<<256, 256>>>(sec, co, p, ntiles, vb, 5); }, reps);
+      const float w5i = time_ms([&] { split5<false, true><<<256, 256>>>(sec, co, p, ntiles, vb, 5); }, reps);
+      const float s5i = time_ms([&] { split5<true, true><<<256, 256>>>(sec, co, p, ntiles, vb, 5); }, reps);
       std::printf(
           "{\"round\": %d, \"set\": %d, \"addr\": \"%p\", \"write1_TBps\": %.3f, \"write1b_TBps\": %.3f, "
-          "\"read1_TBps\": %.3f, \"write5_TBps\": %.3f, \"split5_ms\": %.4f}\n",
+          "\"read1_TBps\": %.3f, \"write5_TBps\": %.3f, \"split5_ms\": %.4f, \"write5il_TBps\": %.3f, "
+          "\"split5il_ms\": %.4f}\n",
           round, i, (void*)p, bytes / (w1 * 1e-3) / 1e12, bytes / (w1b * 1e-3) / 1e12, bytes / (r1 * 1e-3) / 1e12,
-          bytes / (w5 * 1e-3) / 1e12, s5);
+          bytes / (w5 * 1e-3) / 1e12, s5, bytes / (w5i * 1e-3) / 1e12, s5i);
       std::fflush(stdout);
     }
   }
