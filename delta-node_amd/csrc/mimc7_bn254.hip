@@ -20,7 +20,7 @@
 // products of operands below 3 q still leave a result below 2 q: the round
 // sums r + k + c are carry-normalized but not reduced.  Everything stays in
 // Montgomery form between rounds (sums commute with the form);
-// t^7 = ((t^2 t)^2) t: 4 products per round.  Field values cross memory as
+// t^7 = t^4 t^3: 2 squares (45 limb products) and 2 products per round.  Field values cross memory as
 // 8 x 32-bit plain limbs.  The row pass
 // is one lane per row (rows are independent chains); the Merkle pass is one
 // 64-lane workgroup per 128-leaf block, levels handed over through LDS.
@@ -172,6 +172,41 @@ __host__ __device__ inline void mont_mul(uint32_t r[N], const uint32_t a[N], con
   if (geq29(r, k.q29)) sub29_in(r, k.q29);
 }
 
+// Montgomery square r = a^2 R^{-1} mod q (same bounds as mont_mul): the 36
+// off-diagonal products once, against the doubled limb 2 a_j < 2^30 (each
+// column still sums at most 9 products' worth, < 2^59 apiece for the doubled
+// ones), plus the 9 squares — 45 instead of 81 multiply-adds before the
+// reduction.
+__host__ __device__ inline void mont_sqr(uint32_t r[N], const uint32_t a[N], const Consts& k) {
+  uint64_t T[2 * N];
+  uint32_t a2[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) a2[i] = a[i] << 1;
+#pragma unroll
+  for (int i = 0; i < 2 * N; ++i) T[i] = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    T[2 * i] += static_cast<uint64_t>(a[i]) * a[i];
+#pragma unroll
+    for (int j = i + 1; j < N; ++j) T[i + j] += static_cast<uint64_t>(a[i]) * a2[j];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t m = (static_cast<uint32_t>(T[i]) * k.qinv) & kM29;
+#pragma unroll
+    for (int j = 0; j < N; ++j) T[i + j] += static_cast<uint64_t>(m) * k.q29[j];
+    T[i + 1] += T[i] >> 29;
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint64_t v = T[N + i] + c;
+    r[i] = static_cast<uint32_t>(v) & kM29;
+    c = v >> 29;
+  }
+  if (geq29(r, k.q29)) sub29_in(r, k.q29);
+}
+
 // plain 32-bit limbs (< q) -> Montgomery form, and back (canonical)
 __host__ __device__ inline void to_mont(uint32_t r[N], const uint32_t a[L], const Consts& k) {
   uint32_t a29[N];
@@ -193,11 +228,12 @@ __host__ __device__ inline void hash_m(uint32_t out[N], const uint32_t x[N], con
     uint32_t t[N];
     for (int i = 0; i < N; ++i) t[i] = r[i] + key[i] + k.cts[c][i];  // < 3 q: not reduced
     norm29(t);
-    uint32_t t2[N], t3[N], t6[N];
-    mont_mul(t2, t, t, k);
+    // t^7 = t^4 t^3: depth 3 (t^2; t^4 and t^3 independent; their product)
+    uint32_t t2[N], t3[N], t4[N];
+    mont_sqr(t2, t, k);
+    mont_sqr(t4, t2, k);
     mont_mul(t3, t2, t, k);
-    mont_mul(t6, t3, t3, k);
-    mont_mul(r, t6, t, k);
+    mont_mul(r, t4, t3, k);
   }
   for (int i = 0; i < N; ++i) out[i] = r[i];
   addmod29(out, key, k.q29);
@@ -232,7 +268,13 @@ __device__ inline bool float_to_field(double v, double scale, uint32_t out[L], c
   }
   const int limb = sh / 32, bit = sh % 32;
   const unsigned __int128 wide = static_cast<unsigned __int128>(mant) << bit;  // < 2^117
-  for (int i = 0; i < 4 && limb + i < L; ++i) out[limb + i] = static_cast<uint32_t>(wide >> (32 * i));
+  // out[limb + d] = word d of wide (d < 4), by select: a dynamic index into
+  // out would put the array in scratch memory
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int d = i - limb;
+    out[i] = d >= 0 && d < 4 ? static_cast<uint32_t>(wide >> (32 * d)) : 0u;
+  }
   const bool neg = y < 0;
   // a = +-out.  min(a, q - a): negative a -> a (value q - |a|); a > q/2 -> q - a.
   if (neg) {
@@ -351,6 +393,11 @@ __global__ void chain_kernel(const ChainArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint32_t r[N];
   to_mont(r, a.key, a.k);
+  // keep the chain on the VALU: every value here is wave-uniform, and the
+  // compiler would otherwise run the products on the scalar unit (slower:
+  // DESIGN.md 4.6); an asm-defined VGPR value counts as divergent
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(r[i]));
   bool ok = true;
   for (uint64_t i = 0; i < a.n; ++i) {
     uint32_t x[L], xm[N];

@@ -78,7 +78,18 @@ __device__ __forceinline__ void wave_sync() {
 
 // ------------------------------------------------------------------ jumps
 struct JumpJob {
-  int32_t src, poly, dst, pad;  // window indices (dst < 0: padding), jump-table row
+  int32_t src, poly, dst;  // window indices (dst < 0: padding), jump-table row
+  int32_t span;            // words [lo, hi) of g this job evaluates: lo | hi << 16
+};
+
+// A latency-bound level (few jobs: one Horner chain of ~312 steps per jump)
+// splits every jump into P parts over word ranges [lo, hi) of g.  Since
+// g(f) W = sum_k f^(64 k) g_k(f) W, part [lo, hi) evaluates
+// sum_{k in [lo, hi)} f^(64 (k - lo)) g_k(f) (f^(64 lo) W) by Horner over its
+// own words from the window 64 lo words further down W's stream, and the
+// parts' windows XOR to the jump (mt_combine_kernel).
+struct CombineJob {
+  int32_t dst, first, parts, pad;  // dst = XOR of window rows first .. first + parts - 1
 };
 
 struct JumpArgs {
@@ -143,13 +154,28 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return d;
 }
 
+// Compact layout (CT = 1): E[v][j] plain rows of kERow words, j < 684 the
+// T-stream words (44 KB: three workgroups per CU instead of one).  A lane's
+// ten words of chunk t are E[c][u + 64 k], u = lane + 60 - 4 t < 124, k < 10:
+// 64 consecutive words per (t, k) across the wave (conflict-free), 256 B
+// apart in k, i.e. five ds_read2st64_b32 from one address.
+constexpr int kERow = 704;
+constexpr int kECompact = 16 * kERow;
+
 // the ten table words of chunk t (value c) for this lane: off = the lane's row offset for t
+template <int CT>
 __device__ __forceinline__ void table_words(const uint32_t* E, uint32_t off, uint32_t c, uint32_t (&x)[10]) {
-  const uint32_t* p = E + c * kEVWords + off;
+  if constexpr (CT) {
+    const uint32_t* p = E + c * kERow + off;
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const u32x2_t d = *reinterpret_cast<const u32x2_t*>(p + i * kEPair);
-    x[2 * i] = d.x, x[2 * i + 1] = d.y;
+    for (int i = 0; i < 10; ++i) x[i] = p[64 * i];
+  } else {
+    const uint32_t* p = E + c * kEVWords + off;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const u32x2_t d = *reinterpret_cast<const u32x2_t*>(p + i * kEPair);
+      x[2 * i] = d.x, x[2 * i + 1] = d.y;
+    }
   }
 }
 
@@ -157,20 +183,20 @@ __device__ __forceinline__ void table_words(const uint32_t* E, uint32_t off, uin
 // r is Q[(r + K) % 11]): f^64 into the frame's free register, then the 16
 // table windows XORed (two per instruction) into the 624 window words, which
 // now sit at slots 80 .. 703 of the frame (registers 1 .. 10).
-template <int K>
+template <int CT, int K>
 __device__ __forceinline__ void jump_mega(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E,
                                           const uint32_t (&off)[16], uint64_t gw) {
   // the table reads of chunk pair p + 1 are issued before the XORs of pair p
   // (f^64's ds_bpermute first: LDS results return in issue order)
   uint32_t x[2][2][10];
   append64<K>(Q, L);
-  table_words(E, off[0], static_cast<uint32_t>(gw >> 60) & 15u, x[0][0]);
-  table_words(E, off[1], static_cast<uint32_t>(gw >> 56) & 15u, x[0][1]);
+  table_words<CT>(E, off[0], static_cast<uint32_t>(gw >> 60) & 15u, x[0][0]);
+  table_words<CT>(E, off[1], static_cast<uint32_t>(gw >> 56) & 15u, x[0][1]);
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     if (p < 7) {
-      table_words(E, off[2 * p + 2], static_cast<uint32_t>(gw >> (52 - 8 * p)) & 15u, x[(p + 1) & 1][0]);
-      table_words(E, off[2 * p + 3], static_cast<uint32_t>(gw >> (48 - 8 * p)) & 15u, x[(p + 1) & 1][1]);
+      table_words<CT>(E, off[2 * p + 2], static_cast<uint32_t>(gw >> (52 - 8 * p)) & 15u, x[(p + 1) & 1][0]);
+      table_words<CT>(E, off[2 * p + 3], static_cast<uint32_t>(gw >> (48 - 8 * p)) & 15u, x[(p + 1) & 1][1]);
     }
 #pragma unroll
     for (int r = 1; r < 11; ++r)
@@ -178,14 +204,14 @@ __device__ __forceinline__ void jump_mega(uint32_t (&Q)[11], const Lanes& L, con
   }
 }
 
-template <int... ks>
+template <int CT, int... ks>
 __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E,
-                                         const uint32_t (&off)[16], const uint64_t* g, int wi,
+                                         const uint32_t (&off)[16], const uint64_t* g, int wi, int top,
                                          std::integer_sequence<int, ks...>) {
   ((void)[&] {
      const int w = wi - ks;
-     const uint64_t gw = w < kMtPolyWords ? g[w] : 0ull;
-     jump_mega<ks>(Q, L, E, off, gw);
+     const uint64_t gw = w <= top ? g[w] : 0ull;
+     jump_mega<CT, ks>(Q, L, E, off, gw);
    }(),
    ...);
 }
@@ -199,25 +225,57 @@ __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, cons
 //     register, its operands gathered by 3 ds_bpermute;
 //   * the XOR of 16 table windows into the 624 window words (10 registers;
 //     80 ds_read_b64 and 80 v_bitop3 per lane).
+template <int CT>
 __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t E[kEWords];
+  __shared__ __attribute__((aligned(16))) uint32_t E[CT ? kECompact : kEWords];
   __shared__ uint32_t ext[kMtN + 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint32_t j0 = blockIdx.x * kJumpWaves;
   const JumpJob* jp = a.jobs + __builtin_amdgcn_readfirstlane(j0 + wid < a.njobs ? j0 + wid : j0);
   const int32_t poly = __builtin_amdgcn_readfirstlane(jp->poly), dsti = __builtin_amdgcn_readfirstlane(jp->dst);
+  // the workgroup's jobs share the source and lo (one table; job j0 is never padding)
+  const int32_t lo = __builtin_amdgcn_readfirstlane(a.jobs[j0].span) & 0xffff;
+  const int32_t hi = __builtin_amdgcn_readfirstlane(jp->span) >> 16;
   const uint32_t* src = a.wins + static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(a.jobs[j0].src)) * kMtN;
-  // the source stream: words 0..623 of W, then 63 more (each from words <= 459 of W)
-  for (uint32_t i = tid; i < kMtN; i += 64u * kJumpWaves) ext[i] = src[i];
-  __syncthreads();
-  if (tid < 63u) ext[kMtN + tid] = mt_mix(ext[tid], ext[tid + 1], ext[tid + kMtM]);
-  __syncthreads();
-  for (uint32_t e = tid; e < static_cast<uint32_t>(kEWords); e += 64u * kJumpWaves) {
-    const uint32_t wrap = e >= static_cast<uint32_t>(kEWrap) ? 1u : 0u, re = e - wrap * kEWrap;
-    const uint32_t i = re / kEPair, rem = re - i * kEPair;  // pair plane, position in it
-    const uint32_t v = rem / kEVWords, mw = rem - v * kEVWords, m = mw >> 1;
-    // T-stream word; -1 in the gap before the wrap half and the 2 pad words of a plane
-    const int j = (i < 5u && v < 16u) ? 64 * static_cast<int>(2 * i + (mw & 1u) + wrap) + static_cast<int>(m) - 16 : -1;
+  if (lo == 0) {
+    // the source stream: words 0..623 of W, then 63 more (each from words <= 459 of W)
+    for (uint32_t i = tid; i < kMtN; i += 64u * kJumpWaves) ext[i] = src[i];
+    __syncthreads();
+    if (tid < 63u) ext[kMtN + tid] = mt_mix(ext[tid], ext[tid + 1], ext[tid + kMtM]);
+    __syncthreads();
+  } else {
+    // words 64 lo .. 64 lo + 686 of W's stream: step the stream in a 1024-word
+    // LDS ring (the table's space, not yet built), 227 words per step (word
+    // 624 + i needs words i, i + 1, i + 397).  A step writes ring slots
+    // 624..850 past its base and reads 0..623, so one barrier per step.
+    uint32_t* ring = E;
+    for (uint32_t i = tid; i < kMtN; i += 64u * kJumpWaves) ring[i] = src[i];
+    __syncthreads();
+    const uint32_t need = 64u * static_cast<uint32_t>(lo) + 687u;
+    for (uint32_t base = 0; base + kMtN < need; base += kMtN - kMtM) {
+      if (tid < static_cast<uint32_t>(kMtN - kMtM)) {
+        const uint32_t i = base + tid;
+        ring[(i + kMtN) & 1023u] = mt_mix(ring[i & 1023u], ring[(i + 1u) & 1023u], ring[(i + kMtM) & 1023u]);
+      }
+      __syncthreads();
+    }
+    for (uint32_t i = tid; i < 687u; i += 64u * kJumpWaves) ext[i] = ring[(64u * static_cast<uint32_t>(lo) + i) & 1023u];
+    __syncthreads();
+  }
+  for (uint32_t e = tid; e < static_cast<uint32_t>(CT ? kECompact : kEWords); e += 64u * kJumpWaves) {
+    uint32_t v;
+    int j;  // T-stream word of entry e (-1: padding)
+    if constexpr (CT) {
+      v = e / kERow;
+      j = static_cast<int>(e - v * kERow);
+    } else {
+      const uint32_t wrap = e >= static_cast<uint32_t>(kEWrap) ? 1u : 0u, re = e - wrap * kEWrap;
+      const uint32_t i = re / kEPair, rem = re - i * kEPair;  // pair plane, position in it
+      v = rem / kEVWords;
+      const uint32_t mw = rem - v * kEVWords, m = mw >> 1;
+      // -1 in the gap before the wrap half and the 2 pad words of a plane
+      j = (i < 5u && v < 16u) ? 64 * static_cast<int>(2 * i + (mw & 1u) + wrap) + static_cast<int>(m) - 16 : -1;
+    }
     uint32_t x = 0u;
     if (j >= 0 && j < 684) {
 #pragma unroll
@@ -242,19 +300,29 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
     const uint32_t u = lane + 60u - 4u * t;
-    off[t] = (u & 63u) * 2u + (u >> 6) * static_cast<uint32_t>(kEWrap);
+    off[t] = CT ? u : (u & 63u) * 2u + (u >> 6) * static_cast<uint32_t>(kEWrap);
   }
-  int top = kMtPolyWords - 1;
-  while (top > 0 && g[top] == 0ull) --top;  // steps above it leave r = 0
-  // runs of 11 steps (the frame returns to Q[0] after 11); r = 0 before the
-  // first nonzero word, so the run starts with zero words above it
-  for (int wi = top + (10 - top % 11); wi >= 0; wi -= 11)
-    jump_run(Q, L, E, off, g, wi, std::make_integer_sequence<int, 11>{});
+  int top = hi - 1;
+  while (top > lo && g[top] == 0ull) --top;  // steps above it leave r = 0
+  // runs of 11 steps (the frame returns to Q[0] after 11) ending at word lo;
+  // r = 0 before the first nonzero word, so a run starts with zero words above it
+  for (int wi = lo + 11 * ((top - lo) / 11) + 10; wi >= lo + 10; wi -= 11)
+    jump_run<CT>(Q, L, E, off, g, wi, top, std::make_integer_sequence<int, 11>{});
   uint32_t* dst = a.wins + static_cast<uint64_t>(dsti) * kMtN;
 #pragma unroll
   for (int r = 0; r < 11; ++r) {
     const int i = 64 * r + static_cast<int>(lane) - 16;
     if (i >= 0 && i < kMtN) dst[i] = Q[r];
+  }
+}
+
+// The parts of a split level XORed into their jumps' windows.
+__global__ void __launch_bounds__(256) mt_combine_kernel(uint32_t* wins, const CombineJob* cj) {
+  const CombineJob c = cj[blockIdx.x];
+  for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(kMtN); i += 256u) {
+    uint32_t x = 0u;
+    for (int32_t j = 0; j < c.parts; ++j) x ^= wins[static_cast<uint64_t>(c.first + j) * kMtN + i];
+    wins[static_cast<uint64_t>(c.dst) * kMtN + i] = x;
   }
 }
 
@@ -446,39 +514,84 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
 
 uint64_t mt_subs(uint64_t ncoef) { return (ncoef + kCoefPerSub - 1) / kCoefPerSub; }
 
-// Jump jobs of one level, grouped by source window in workgroups of
-// kJumpWaves jobs (padding: dst -1).
-void push_group(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd) {
-  for (size_t i = 0; i < pd.size(); ++i) jobs.push_back({src, pd[i].first, pd[i].second, 0});
-  while (jobs.size() % kJumpWaves) jobs.push_back({src, 0, -1, 0});
+constexpr int32_t kFullSpan = kMtPolyWords << 16;  // words [0, 312)
+constexpr int kMaxParts = 16;
+constexpr uint64_t kPartRows = 512;  // part windows of one split level (jobs x parts <= 512)
+constexpr uint64_t kCombineCap = 64 + 256;  // split jumps of levels A and C
+
+// Jump jobs of one level, grouped by source window (and part) in workgroups
+// of kJumpWaves jobs (padding: dst -1).
+void push_group(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd,
+                int32_t span) {
+  for (size_t i = 0; i < pd.size(); ++i) jobs.push_back({src, pd[i].first, pd[i].second, span});
+  while (jobs.size() % kJumpWaves) jobs.push_back({src, 0, -1, span});
 }
 
 // split a source's jobs into groups of at most `per` (fewer jumps per
-// workgroup = less LDS traffic per CU: the first level is latency-bound)
+// workgroup = less LDS traffic per CU: a latency-bound level)
 void push_groups(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd,
-                 size_t per) {
+                 size_t per, int32_t span = kFullSpan) {
   for (size_t i = 0; i < pd.size(); i += per)
-    push_group(jobs, src, std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + per)));
+    push_group(jobs, src, std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + per)),
+               span);
 }
 
-// Levels for windows 1 .. S-1 (s - 1 = 4096 c + 64 a + b; row S holds W_idx):
-// A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a) = C_c(W(1 + 64 a));
-// B: W(base + b) = B_b(W(base)).
-void build_levels(uint64_t S, std::vector<JumpJob> lv[3]) {
+// One latency-bound level: (source, [(poly, dst)]) lists.  Few jumps (< 256)
+// are split into P parts (jumps x P <= 512, workgroups of 2 jobs: every CU
+// busy, ~312 / P Horner steps each) written to part rows prow0 .. and XORed
+// into their windows by `comb`; otherwise 2 whole jumps per workgroup.
+void push_level(std::vector<JumpJob>& jobs, std::vector<CombineJob>& comb,
+                const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs, int32_t prow0) {
+  size_t n = 0;
+  for (auto& sp : srcs) n += sp.second.size();
+  const int P = n == 0 || n >= 256 ? 1 : static_cast<int>(std::min<size_t>(kMaxParts, kPartRows / n));
+  if (P == 1) {
+    for (auto& sp : srcs) push_groups(jobs, sp.first, sp.second, 2);
+    return;
+  }
+  int32_t row = prow0;
+  for (auto& sp : srcs)
+    for (auto& pd : sp.second) {
+      comb.push_back({pd.second, row, P, 0});
+      row += P;
+    }
+  for (int j = 0; j < P; ++j) {
+    const int32_t lo = kMtPolyWords * j / P, hi = kMtPolyWords * (j + 1) / P;
+    row = prow0 + j;
+    for (auto& sp : srcs) {
+      std::vector<std::pair<int32_t, int32_t>> pd;
+      for (auto& q : sp.second) {
+        pd.push_back({q.first, row});
+        row += P;
+      }
+      push_groups(jobs, sp.first, pd, 2, lo | hi << 16);
+    }
+  }
+}
+
+// Levels for windows 1 .. S-1 (s - 1 = 4096 c + 64 a + b; row S holds W_idx;
+// part rows from S + 1): A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a)
+// = C_c(W(1 + 64 a)); B: W(base + b) = B_b(W(base)).
+void build_levels(uint64_t S, std::vector<JumpJob> lv[3], std::vector<CombineJob> cb[3]) {
   const uint64_t R = kMtJumpRadix;
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
+  const int32_t prow0 = static_cast<int32_t>(S + 1);
   {
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t a = 0; a <= last / R && a < R; ++a)
       pd.push_back({kMtRowA + static_cast<int32_t>(a), static_cast<int32_t>(1 + R * a)});
-    push_groups(lv[0], static_cast<int32_t>(S), pd, 2);
+    push_level(lv[0], cb[0], {{static_cast<int32_t>(S), pd}}, prow0);
   }
-  for (uint64_t a = 0; a < R && R * a <= last; ++a) {  // C: per source W(1 + 64 a), its c digits
-    std::vector<std::pair<int32_t, int32_t>> pd;
-    for (uint64_t c = 1; c < R && R * R * c + R * a <= last; ++c)
-      pd.push_back({kMtRowC + static_cast<int32_t>(c), static_cast<int32_t>(1 + R * R * c + R * a)});
-    push_groups(lv[1], static_cast<int32_t>(1 + R * a), pd, 2);
+  {
+    std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>> srcs;
+    for (uint64_t a = 0; a < R && R * a <= last; ++a) {  // C: per source W(1 + 64 a), its c digits
+      std::vector<std::pair<int32_t, int32_t>> pd;
+      for (uint64_t c = 1; c < R && R * R * c + R * a <= last; ++c)
+        pd.push_back({kMtRowC + static_cast<int32_t>(c), static_cast<int32_t>(1 + R * R * c + R * a)});
+      if (!pd.empty()) srcs.push_back({static_cast<int32_t>(1 + R * a), pd});
+    }
+    push_level(lv[1], cb[1], srcs, prow0);
   }
   for (uint64_t base = 0; base <= last; base += R) {  // B: per source W(1 + base)
     std::vector<std::pair<int32_t, int32_t>> pd;
@@ -488,8 +601,9 @@ void build_levels(uint64_t S, std::vector<JumpJob> lv[3]) {
   }
 }
 
-// >= the three levels with padding (levels A and C: 2 jobs per workgroup of 8)
-uint64_t jobs_cap(uint64_t S) { return 2 * S + 4 * 64 * kJumpWaves + 1024; }
+// >= the three levels with padding (split levels: jumps x parts <= 512 jobs,
+// 2 per workgroup of 8 -> <= 2048 entries each)
+uint64_t jobs_cap(uint64_t S) { return 2 * S + 4 * 64 * kJumpWaves + 2 * 4 * kPartRows + 1024; }
 
 constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
 
@@ -500,7 +614,7 @@ using namespace dn;
 
 extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
   const uint64_t S = tm1 > 0 ? mt_subs(n_elem * static_cast<uint64_t>(tm1)) : 0;
-  return kHead + (S + 1) * kMtN * 4 + jobs_cap(S) * sizeof(JumpJob);
+  return kHead + (S + 1 + kPartRows) * kMtN * 4 + jobs_cap(S) * sizeof(JumpJob) + kCombineCap * sizeof(CombineJob);
 }
 
 namespace dn {
@@ -541,38 +655,56 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   }
 
   // scratch: head (flag at 0, final array at 256) | windows 0..S (row 0 the
-  // caller's array, row S that array advanced idx words) | jump jobs.  Two
-  // copies: [zeroed head, row 0] and [row S, jobs].
+  // caller's array, row S that array advanced idx words) | part rows (split
+  // levels) | jump jobs | combine jobs.  Two copies: [zeroed head, row 0] and
+  // [jobs, combine jobs]; row S is written by the host between them.
   std::vector<JumpJob> lv[3];
-  build_levels(S, lv);
+  std::vector<CombineJob> cb[3];
+  build_levels(S, lv, cb);
   const uint64_t njobs = lv[0].size() + lv[1].size() + lv[2].size();
-  if (njobs > jobs_cap(S)) return set_error(DN_ERR_ARG, "%s: job table overflow", name);
+  const uint64_t ncomb = cb[0].size() + cb[1].size() + cb[2].size();
+  if (njobs > jobs_cap(S) || ncomb > kCombineCap) return set_error(DN_ERR_ARG, "%s: job table overflow", name);
   std::vector<uint32_t> st1(kHead / 4 + kMtN, 0u);
   std::memcpy(st1.data() + kHead / 4, mt_state, kMtN * 4);
-  std::vector<uint32_t> st2(kMtN + njobs * sizeof(JumpJob) / 4);
+  std::vector<uint32_t> st2(kMtN);
   mt_advance_window(mt_state, static_cast<uint64_t>(idx), st2.data());
+  std::vector<uint32_t> st3((njobs * sizeof(JumpJob) + ncomb * sizeof(CombineJob)) / 4);
   {
-    uint64_t o = kMtN;
+    uint64_t o = 0;
     for (auto& l : lv) {
-      std::memcpy(st2.data() + o, l.data(), l.size() * sizeof(JumpJob));
+      std::memcpy(st3.data() + o, l.data(), l.size() * sizeof(JumpJob));
       o += l.size() * sizeof(JumpJob) / 4;
+    }
+    for (auto& c : cb) {
+      std::memcpy(st3.data() + o, c.data(), c.size() * sizeof(CombineJob));
+      o += c.size() * sizeof(CombineJob) / 4;
     }
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
   uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead);
-  JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead + (S + 1) * kMtN * 4);
+  JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead + (S + 1 + kPartRows) * kMtN * 4);
+  CombineJob* dcomb = reinterpret_cast<CombineJob*>(djobs + njobs);
   hipError_t err = hipMemcpyAsync(sc, st1.data(), st1.size() * 4, hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipMemcpyAsync(dwin + S * kMtN, st2.data(), st2.size() * 4, hipMemcpyHostToDevice, s);
+  if (err == hipSuccess && !st3.empty())
+    err = hipMemcpyAsync(djobs, st3.data(), st3.size() * 4, hipMemcpyHostToDevice, s);
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
-  uint64_t off = 0;
-  for (auto& l : lv) {
-    if (!l.empty()) {
-      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.size())};
-      hipLaunchKernelGGL(mt_jump_kernel, dim3(static_cast<uint32_t>(l.size() / kJumpWaves)), dim3(64 * kJumpWaves), 0, s,
-                         ja);
+  // table layout of the jump kernel: DN_MT_JUMP_LAYOUT=1 (tuning build) the compact rows
+  const char* jl = tune_env("DN_MT_JUMP_LAYOUT");
+  const bool compact = jl && jl[0] == '1';
+  uint64_t off = 0, coff = 0;
+  for (int k = 0; k < 3; ++k) {
+    if (!lv[k].empty()) {
+      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(lv[k].size())};
+      const dim3 grid(static_cast<uint32_t>(lv[k].size() / kJumpWaves)), block(64 * kJumpWaves);
+      if (compact) hipLaunchKernelGGL(mt_jump_kernel<1>, grid, block, 0, s, ja);
+      else hipLaunchKernelGGL(mt_jump_kernel<0>, grid, block, 0, s, ja);
     }
-    off += l.size();
+    if (!cb[k].empty())
+      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(cb[k].size())), dim3(256), 0, s, dwin, dcomb + coff);
+    off += lv[k].size();
+    coff += cb[k].size();
   }
   GenArgs ga{};
   ga.wins = dwin;
