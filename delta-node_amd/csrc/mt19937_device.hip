@@ -154,28 +154,13 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return d;
 }
 
-// Compact layout (CT = 1): E[v][j] plain rows of kERow words, j < 684 the
-// T-stream words (44 KB: three workgroups per CU instead of one).  A lane's
-// ten words of chunk t are E[c][u + 64 k], u = lane + 60 - 4 t < 124, k < 10:
-// 64 consecutive words per (t, k) across the wave (conflict-free), 256 B
-// apart in k, i.e. five ds_read2st64_b32 from one address.
-constexpr int kERow = 704;
-constexpr int kECompact = 16 * kERow;
-
 // the ten table words of chunk t (value c) for this lane: off = the lane's row offset for t
-template <int CT>
 __device__ __forceinline__ void table_words(const uint32_t* E, uint32_t off, uint32_t c, uint32_t (&x)[10]) {
-  if constexpr (CT) {
-    const uint32_t* p = E + c * kERow + off;
+  const uint32_t* p = E + c * kEVWords + off;
 #pragma unroll
-    for (int i = 0; i < 10; ++i) x[i] = p[64 * i];
-  } else {
-    const uint32_t* p = E + c * kEVWords + off;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const u32x2_t d = *reinterpret_cast<const u32x2_t*>(p + i * kEPair);
-      x[2 * i] = d.x, x[2 * i + 1] = d.y;
-    }
+  for (int i = 0; i < 5; ++i) {
+    const u32x2_t d = *reinterpret_cast<const u32x2_t*>(p + i * kEPair);
+    x[2 * i] = d.x, x[2 * i + 1] = d.y;
   }
 }
 
@@ -183,20 +168,20 @@ __device__ __forceinline__ void table_words(const uint32_t* E, uint32_t off, uin
 // r is Q[(r + K) % 11]): f^64 into the frame's free register, then the 16
 // table windows XORed (two per instruction) into the 624 window words, which
 // now sit at slots 80 .. 703 of the frame (registers 1 .. 10).
-template <int CT, int K>
+template <int K>
 __device__ __forceinline__ void jump_mega(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E,
                                           const uint32_t (&off)[16], uint64_t gw) {
   // the table reads of chunk pair p + 1 are issued before the XORs of pair p
   // (f^64's ds_bpermute first: LDS results return in issue order)
   uint32_t x[2][2][10];
   append64<K>(Q, L);
-  table_words<CT>(E, off[0], static_cast<uint32_t>(gw >> 60) & 15u, x[0][0]);
-  table_words<CT>(E, off[1], static_cast<uint32_t>(gw >> 56) & 15u, x[0][1]);
+  table_words(E, off[0], static_cast<uint32_t>(gw >> 60) & 15u, x[0][0]);
+  table_words(E, off[1], static_cast<uint32_t>(gw >> 56) & 15u, x[0][1]);
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
     if (p < 7) {
-      table_words<CT>(E, off[2 * p + 2], static_cast<uint32_t>(gw >> (52 - 8 * p)) & 15u, x[(p + 1) & 1][0]);
-      table_words<CT>(E, off[2 * p + 3], static_cast<uint32_t>(gw >> (48 - 8 * p)) & 15u, x[(p + 1) & 1][1]);
+      table_words(E, off[2 * p + 2], static_cast<uint32_t>(gw >> (52 - 8 * p)) & 15u, x[(p + 1) & 1][0]);
+      table_words(E, off[2 * p + 3], static_cast<uint32_t>(gw >> (48 - 8 * p)) & 15u, x[(p + 1) & 1][1]);
     }
 #pragma unroll
     for (int r = 1; r < 11; ++r)
@@ -204,14 +189,14 @@ __device__ __forceinline__ void jump_mega(uint32_t (&Q)[11], const Lanes& L, con
   }
 }
 
-template <int CT, int... ks>
+template <int... ks>
 __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E,
                                          const uint32_t (&off)[16], const uint64_t* g, int wi, int top,
                                          std::integer_sequence<int, ks...>) {
   ((void)[&] {
      const int w = wi - ks;
      const uint64_t gw = w <= top ? g[w] : 0ull;
-     jump_mega<CT, ks>(Q, L, E, off, gw);
+     jump_mega<ks>(Q, L, E, off, gw);
    }(),
    ...);
 }
@@ -225,9 +210,8 @@ __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, cons
 //     register, its operands gathered by 3 ds_bpermute;
 //   * the XOR of 16 table windows into the 624 window words (10 registers;
 //     80 ds_read_b64 and 80 v_bitop3 per lane).
-template <int CT>
 __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t E[CT ? kECompact : kEWords];
+  __shared__ __attribute__((aligned(16))) uint32_t E[kEWords];
   __shared__ uint32_t ext[kMtN + 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint32_t j0 = blockIdx.x * kJumpWaves;
@@ -262,20 +246,12 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
     for (uint32_t i = tid; i < 687u; i += 64u * kJumpWaves) ext[i] = ring[(64u * static_cast<uint32_t>(lo) + i) & 1023u];
     __syncthreads();
   }
-  for (uint32_t e = tid; e < static_cast<uint32_t>(CT ? kECompact : kEWords); e += 64u * kJumpWaves) {
-    uint32_t v;
-    int j;  // T-stream word of entry e (-1: padding)
-    if constexpr (CT) {
-      v = e / kERow;
-      j = static_cast<int>(e - v * kERow);
-    } else {
-      const uint32_t wrap = e >= static_cast<uint32_t>(kEWrap) ? 1u : 0u, re = e - wrap * kEWrap;
-      const uint32_t i = re / kEPair, rem = re - i * kEPair;  // pair plane, position in it
-      v = rem / kEVWords;
-      const uint32_t mw = rem - v * kEVWords, m = mw >> 1;
-      // -1 in the gap before the wrap half and the 2 pad words of a plane
-      j = (i < 5u && v < 16u) ? 64 * static_cast<int>(2 * i + (mw & 1u) + wrap) + static_cast<int>(m) - 16 : -1;
-    }
+  for (uint32_t e = tid; e < static_cast<uint32_t>(kEWords); e += 64u * kJumpWaves) {
+    const uint32_t wrap = e >= static_cast<uint32_t>(kEWrap) ? 1u : 0u, re = e - wrap * kEWrap;
+    const uint32_t i = re / kEPair, rem = re - i * kEPair;  // pair plane, position in it
+    const uint32_t v = rem / kEVWords, mw = rem - v * kEVWords, m = mw >> 1;
+    // T-stream word; -1 in the gap before the wrap half and the 2 pad words of a plane
+    const int j = (i < 5u && v < 16u) ? 64 * static_cast<int>(2 * i + (mw & 1u) + wrap) + static_cast<int>(m) - 16 : -1;
     uint32_t x = 0u;
     if (j >= 0 && j < 684) {
 #pragma unroll
@@ -300,14 +276,14 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
     const uint32_t u = lane + 60u - 4u * t;
-    off[t] = CT ? u : (u & 63u) * 2u + (u >> 6) * static_cast<uint32_t>(kEWrap);
+    off[t] = (u & 63u) * 2u + (u >> 6) * static_cast<uint32_t>(kEWrap);
   }
   int top = hi - 1;
   while (top > lo && g[top] == 0ull) --top;  // steps above it leave r = 0
   // runs of 11 steps (the frame returns to Q[0] after 11) ending at word lo;
   // r = 0 before the first nonzero word, so a run starts with zero words above it
   for (int wi = lo + 11 * ((top - lo) / 11) + 10; wi >= lo + 10; wi -= 11)
-    jump_run<CT>(Q, L, E, off, g, wi, top, std::make_integer_sequence<int, 11>{});
+    jump_run(Q, L, E, off, g, wi, top, std::make_integer_sequence<int, 11>{});
   uint32_t* dst = a.wins + static_cast<uint64_t>(dsti) * kMtN;
 #pragma unroll
   for (int r = 0; r < 11; ++r) {
@@ -690,16 +666,12 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   if (err == hipSuccess && !st3.empty())
     err = hipMemcpyAsync(djobs, st3.data(), st3.size() * 4, hipMemcpyHostToDevice, s);
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
-  // table layout of the jump kernel: DN_MT_JUMP_LAYOUT=1 (tuning build) the compact rows
-  const char* jl = tune_env("DN_MT_JUMP_LAYOUT");
-  const bool compact = jl && jl[0] == '1';
   uint64_t off = 0, coff = 0;
   for (int k = 0; k < 3; ++k) {
     if (!lv[k].empty()) {
       const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(lv[k].size())};
-      const dim3 grid(static_cast<uint32_t>(lv[k].size() / kJumpWaves)), block(64 * kJumpWaves);
-      if (compact) hipLaunchKernelGGL(mt_jump_kernel<1>, grid, block, 0, s, ja);
-      else hipLaunchKernelGGL(mt_jump_kernel<0>, grid, block, 0, s, ja);
+      hipLaunchKernelGGL(mt_jump_kernel, dim3(static_cast<uint32_t>(lv[k].size() / kJumpWaves)), dim3(64 * kJumpWaves),
+                         0, s, ja);
     }
     if (!cb[k].empty())
       hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(cb[k].size())), dim3(256), 0, s, dwin, dcomb + coff);
