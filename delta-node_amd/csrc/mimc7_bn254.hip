@@ -337,45 +337,56 @@ struct MerkleArgs {
   uint32_t* roots;         // [blocks][8] plain
 };
 
-// One workgroup of 64 lanes per 128-leaf block: level sizes 64, 32, ..., 1.
-__global__ void __launch_bounds__(64) merkle_kernel(const MerkleArgs a) {
-  __shared__ uint32_t s[64][N];
+// BPW 128-leaf blocks per workgroup of 64 BPW lanes; level sizes 64, 32,
+// ..., 1 nodes per block.  The nodes of a level are packed onto the first
+// lanes (thread t -> block t / w, node t % w), so every active wave is full
+// until a level has fewer than 64 nodes in the workgroup: 33 wave-levels per
+// 16 blocks instead of 7 per block (many blocks); BPW = 1 when there are few
+// blocks (each level is then one hash-pair latency per wave either way).
+template <int BPW>
+__global__ void __launch_bounds__(64 * BPW) merkle_kernel(const MerkleArgs a, uint64_t blocks) {
+  __shared__ uint32_t s[64 * BPW][N];
   const uint32_t t = threadIdx.x;
-  const uint32_t* lv = a.leaves + static_cast<uint64_t>(blockIdx.x) * 128 * L;
+  const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * BPW;
   uint32_t key[N];
   {
     const uint32_t two[L] = {2, 0, 0, 0, 0, 0, 0, 0};
     to_mont(key, two, a.k);
   }
-  uint32_t l[L], r[L], lm[N], rm[N], acc[N];
-  for (int i = 0; i < L; ++i) {
-    l[i] = lv[(2 * t) * L + i];
-    r[i] = lv[(2 * t + 1) * L + i];
+  if (b0 + t / 64 < blocks) {
+    const uint32_t* lv = a.leaves + (b0 + t / 64) * 128 * L;
+    const uint32_t j = t % 64;
+    uint32_t l[L], r[L], lm[N], rm[N], acc[N];
+    for (int i = 0; i < L; ++i) {
+      l[i] = lv[(2 * j) * L + i];
+      r[i] = lv[(2 * j + 1) * L + i];
+    }
+    to_mont(lm, l, a.k);
+    to_mont(rm, r, a.k);
+    for (int i = 0; i < N; ++i) acc[i] = key[i];
+    arr_step(acc, lm, a.k);
+    arr_step(acc, rm, a.k);
+    for (int i = 0; i < N; ++i) s[t][i] = acc[i];  // Montgomery form from here on; block b at s[64 b ..]
   }
-  to_mont(lm, l, a.k);
-  to_mont(rm, r, a.k);
-  for (int i = 0; i < N; ++i) acc[i] = key[i];
-  arr_step(acc, lm, a.k);
-  arr_step(acc, rm, a.k);
-  for (int i = 0; i < N; ++i) s[t][i] = acc[i];  // Montgomery form from here on
   __syncthreads();
   for (uint32_t width = 32; width >= 1; width >>= 1) {
     uint32_t nxt[N];
-    const bool act = t < width;
+    const uint32_t b = t / width, j = t % width;
+    const bool act = t < BPW * width && b0 + b < blocks;
     if (act) {
       for (int i = 0; i < N; ++i) nxt[i] = key[i];
-      arr_step(nxt, s[2 * t], a.k);
-      arr_step(nxt, s[2 * t + 1], a.k);
+      arr_step(nxt, s[64 * b + 2 * j], a.k);
+      arr_step(nxt, s[64 * b + 2 * j + 1], a.k);
     }
     __syncthreads();
     if (act)
-      for (int i = 0; i < N; ++i) s[t][i] = nxt[i];
+      for (int i = 0; i < N; ++i) s[64 * b + j][i] = nxt[i];
     __syncthreads();
   }
-  if (t == 0) {
+  if (t < BPW && b0 + t < blocks) {
     uint32_t out[L];
-    from_mont(out, s[0], a.k);
-    for (int i = 0; i < L; ++i) a.roots[static_cast<uint64_t>(blockIdx.x) * L + i] = out[i];
+    from_mont(out, s[64 * t], a.k);
+    for (int i = 0; i < L; ++i) a.roots[(b0 + t) * L + i] = out[i];
   }
 }
 
@@ -518,8 +529,14 @@ extern "C" int dn_mimc7_merkle_blocks(const uint32_t* leaves, uint64_t blocks, u
   consts(a.k);
   a.leaves = leaves;
   a.roots = roots;
-  hipLaunchKernelGGL(merkle_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(64), 0,
-                     static_cast<hipStream_t>(stream), a);
+  // blocks per workgroup: pack levels across blocks once there are >= 512 workgroups' worth
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  if (blocks >= 16 * 512)
+    hipLaunchKernelGGL(merkle_kernel<16>, dim3(static_cast<uint32_t>((blocks + 15) / 16)), dim3(64 * 16), 0, s, a, blocks);
+  else if (blocks >= 4 * 512)
+    hipLaunchKernelGGL(merkle_kernel<4>, dim3(static_cast<uint32_t>((blocks + 3) / 4)), dim3(64 * 4), 0, s, a, blocks);
+  else
+    hipLaunchKernelGGL(merkle_kernel<1>, dim3(static_cast<uint32_t>(blocks)), dim3(64), 0, s, a, blocks);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_mimc7_merkle_blocks: %s", hipGetErrorString(err));
   return DN_OK;

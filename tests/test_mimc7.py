@@ -130,3 +130,27 @@ def test_gpu_vs_oracle_random():
     data[:, -1] = np.random.default_rng(4).integers(0, 2, 300)
     data[5, 2] = -3.3e20
     assert mimc7.calc_data_commitment(data) == om.data_commitment(data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("blocks", [2048 + 3, 8192 + 5])
+def test_gpu_packed_merkle_blocks_equal_single_blocks(blocks):
+    """Many blocks take the packed Merkle kernel (4 or 16 blocks per
+    workgroup, levels packed onto full waves, a partial last workgroup): each
+    root equals the commitment of its 128 rows alone (one block, the
+    one-block-per-workgroup kernel the oracle pins), for blocks at the start,
+    around workgroup boundaries and at the end."""
+    import torch
+
+    from delta_node.utils import mimc7
+
+    rows = blocks * 128 - 77  # the last block is zero-padded
+    rng = np.random.default_rng(blocks)
+    data = rng.standard_normal((rows, 6))
+    data[:, -1] = rng.integers(0, 2, rows)
+    dev = torch.device("cuda", 0)
+    roots = mimc7.calc_data_commitment(torch.from_numpy(data).to(dev))
+    assert len(roots) == blocks
+    for b in sorted({0, 1, 3, 4, 15, 16, 17, blocks // 2, blocks - 6, blocks - 2, blocks - 1}):
+        one = mimc7.calc_data_commitment(torch.from_numpy(data[128 * b:128 * (b + 1)]).to(dev))
+        assert roots[b] == one[0], b
