@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Fixed cost of make_shares_vec's fused MT19937 draw + split (the drop-in
+vector path) per call: wall time per call at several sizes, 3-of-5, shares
+preallocated.  Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "delta-node_amd"))
+
+import torch  # noqa: E402
+
+from delta_node.crypto import shamir  # noqa: E402
+from delta_node.crypto.shamir import field  # noqa: E402
+
+dev = torch.device("cuda", 0)
+out = {}
+for lg in (8, 12, 16, 20, 24):
+    N = 1 << lg
+    sec = torch.randint(-(1 << 62), 1 << 62, (N,), dtype=torch.int64, device=dev)
+    sh = torch.empty((5, field.vec_bytes(N)), dtype=torch.uint8, device=dev)
+    ss = shamir.SecretShare(3)
+    ss.random.seed(lg)
+    for _ in range(3):
+        ss.make_shares_vec(sec, 5, out=sh)
+    torch.cuda.synchronize()
+    reps = 50 if lg < 24 else 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ss.make_shares_vec(sec, 5, out=sh)
+    torch.cuda.synchronize()
+    out[f"2^{lg}"] = (time.perf_counter() - t0) / reps * 1e3
+print(json.dumps({"make_shares_vec_ms_per_call": out}))
