@@ -711,13 +711,30 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
         del co, want
     fm, um = min(fused), min(unfused)
     words = 17 * 2 * n
+    # smaller vectors take shorter MT substreams (2^10 / 2^12 / 2^14 draws: dn_mt19937_split_device)
+    by_size = {}
+    for lg in (12, 16, 20, 22):
+        m = 1 << lg
+        ss = shamir.SecretShare(3)
+        ss.random.seed(lg)
+        sm, om = sec[:m], out[:, : field.vec_bytes(m)]
+        o2 = torch.empty((5, field.vec_bytes(m)), dtype=torch.uint8, device=dev)
+        for _ in range(2):
+            ss.make_shares_vec(sm, 5, out=o2)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            ss.make_shares_vec(sm, 5, out=o2)
+        torch.cuda.synchronize()
+        by_size[f"2^{lg}"] = (time.perf_counter() - t0) / 10 * 1e3
+        del om, o2
     return {"workload": f"make_shares_vec(2^{log2n} int64, 5) on SecretShare(3), coefficients = the reference's "
                         "MT19937 draws (shamir.py:59-61), bit-exact", "unit": "elements/s",
             "fused_ms": fm * 1e3, "fused_elems_per_s": n / fm, "draw_then_split_ms": um * 1e3,
             "draw_then_split_elems_per_s": n / um, "mt_words_per_s_fused": words / fm,
             "roofline_fused": roof("hbm", n * (8 + 5 * 66) / fm / 1e9,
                                    "8 B secret + 5 x 66 B shares per element (wall time of the whole call)"),
-            "equal_draw_then_split_and_state": ok}
+            "equal_draw_then_split_and_state": ok, "fused_ms_by_size": by_size}
 
 
 def byte_api_row(budget_s: float = 2.0) -> dict:

@@ -5,8 +5,9 @@
 // 1 + getrandbits(521), redrawn while >= p-1; getrandbits(521) is 17 MT19937
 // words, little-endian, the last >> 23.  dn_mt19937_draw_coeffs (host_m521.cpp)
 // restates that stream sequentially; this file produces the same values on the
-// device by cutting the word stream into S substreams of L = 17 * 2^14 words
-// (2^14 whole draws each), all on the GPU:
+// device by cutting the word stream into S substreams of L = 17 * 2^k words
+// (2^k whole draws each; k = 14 from 2^24 coefficients, 12 from 2^21, else
+// 10), all on the GPU:
 //
 //  * jump kernel: the MT window at the start of every substream by
 //    jump-ahead, g(f)(W) with g = x^J mod P (P the characteristic polynomial
@@ -42,16 +43,32 @@ namespace dn {
 namespace {
 
 #include "mt19937_jump.inc"
+#include "mt19937_jump_short.inc"
 
-__device__ const uint64_t kMtPolysDev[kMtJumpRows][kMtPolyWords] = DN_MT_JUMP_POLYS;
+// Substream lengths: L_k = 17 * 2^k words (2^k whole draws), k = 10, 12, 14,
+// one jump table each (rows A, C, B as in mt19937_jump.inc).  A draw of ncoef
+// coefficients uses one k for all its substreams (mt_sub_len): long
+// substreams for big draws (fewer jumps), short ones for small draws (a
+// substream's generation is one wave's sequential run: ~48 ns per draw, so
+// 2^14 draws cost ~0.8 ms whatever the vector size).
+constexpr int kMtLens = 3;
+constexpr int kMtLenLog2[kMtLens] = {10, 12, 14};
+__device__ const uint64_t kMtPolysDev[kMtLens][kMtJumpRows][kMtPolyWords] = {
+    DN_MT_JUMP_POLYS_L10, DN_MT_JUMP_POLYS_L12, DN_MT_JUMP_POLYS};
+static_assert(kMtJumpL10 == 17ull << 10 && kMtJumpL12 == 17ull << 12 && kMtJumpL == 17ull << 14, "table lengths");
 
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kMtN = 624, kMtM = 397;
 constexpr uint32_t kMtA = 0x9908b0dfu, kMtUp = 0x80000000u, kMtLo = 0x7fffffffu;
-constexpr uint64_t kCoefPerSub = kMtJumpL / 17;            // 2^14 draws per substream
-static_assert(kMtJumpL % 17 == 0, "substreams hold whole 17-word draws");
+
+// table index of the substream length of a draw of ncoef coefficients:
+// 2^14 draws from 2^24 coefficients, 2^12 from 2^21, else 2^10 (at least
+// ~2048 substreams for the big draws; a few hundred jumps and a short
+// generation run below)
+inline int mt_sub_len(uint64_t ncoef) { return ncoef >= (1ull << 24) ? 2 : ncoef >= (1ull << 21) ? 1 : 0; }
+inline uint64_t mt_sub_draws(int ki) { return 1ull << kMtLenLog2[ki]; }
 
 __host__ __device__ inline uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
@@ -262,7 +279,7 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
   __syncthreads();
   if (j0 + wid >= a.njobs || dsti < 0) return;
 
-  const uint64_t* g = kMtPolysDev[poly];
+  const uint64_t* g = &kMtPolysDev[0][0][0] + static_cast<uint64_t>(poly) * kMtPolyWords;  // poly = table * rows + row
   uint32_t Q[11];
 #pragma unroll
   for (int r = 0; r < 11; ++r) Q[r] = 0u;
@@ -309,6 +326,7 @@ struct GenArgs {
   uint32_t* flag;        // != 0: a draw was rejected
   uint32_t* fin;         // CPython's final array (the final-state wave)
   uint64_t ncoef, vb;
+  uint64_t sub_draws;    // draws per substream (2^k)
   uint64_t tm1_magic;    // ceil(2^32 / tm1): x / tm1 = (x * magic) >> 32 for x < 2^16
   uint32_t S;            // substreams
   uint32_t idx;          // CPython index: stream words 0..623-idx are temper(window0[idx..])
@@ -458,8 +476,8 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   }
   uint32_t* R = s_ring;
   const uint32_t group = a.ring / 2u;                            // words per emission group
-  const uint64_t k0 = static_cast<uint64_t>(sub) * kCoefPerSub;  // first draw of this substream
-  const uint32_t nloc = static_cast<uint32_t>(a.ncoef - k0 < kCoefPerSub ? a.ncoef - k0 : kCoefPerSub);
+  const uint64_t k0 = static_cast<uint64_t>(sub) * a.sub_draws;  // first draw of this substream
+  const uint32_t nloc = static_cast<uint32_t>(a.ncoef - k0 < a.sub_draws ? a.ncoef - k0 : a.sub_draws);
   const uint32_t gdraws = T ? 64u * (T - 1) : 64u;  // draws per group
   const uint32_t ngroups = (nloc + gdraws - 1u) / gdraws;
   const uint64_t qb = k0 / static_cast<uint64_t>(a.tm1);
@@ -488,12 +506,15 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   }
 }
 
-uint64_t mt_subs(uint64_t ncoef) { return (ncoef + kCoefPerSub - 1) / kCoefPerSub; }
+uint64_t mt_subs(uint64_t ncoef) {
+  const uint64_t d = mt_sub_draws(mt_sub_len(ncoef));
+  return (ncoef + d - 1) / d;
+}
 
 constexpr int32_t kFullSpan = kMtPolyWords << 16;  // words [0, 312)
 constexpr int kMaxParts = 16;
 constexpr uint64_t kPartRows = 512;  // part windows of one split level (jobs x parts <= 512)
-constexpr uint64_t kCombineCap = 64 + 256;  // split jumps of levels A and C
+constexpr uint64_t kCombineCap = 64 + 256 + 256;  // split jumps of levels A, C and B
 
 // Jump jobs of one level, grouped by source window (and part) in workgroups
 // of kJumpWaves jobs (padding: dst -1).
@@ -515,14 +536,17 @@ void push_groups(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std:
 // One latency-bound level: (source, [(poly, dst)]) lists.  Few jumps (< 256)
 // are split into P parts (jumps x P <= 512, workgroups of 2 jobs: every CU
 // busy, ~312 / P Horner steps each) written to part rows prow0 .. and XORed
-// into their windows by `comb`; otherwise 2 whole jumps per workgroup.
+// into their windows by `comb`; otherwise `whole_per` whole jumps per workgroup.
 void push_level(std::vector<JumpJob>& jobs, std::vector<CombineJob>& comb,
-                const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs, int32_t prow0) {
+                const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs, int32_t prow0,
+                size_t whole_per) {
   size_t n = 0;
   for (auto& sp : srcs) n += sp.second.size();
   const int P = n == 0 || n >= 256 ? 1 : static_cast<int>(std::min<size_t>(kMaxParts, kPartRows / n));
   if (P == 1) {
-    for (auto& sp : srcs) push_groups(jobs, sp.first, sp.second, 2);
+    // whole jumps: at most whole_per per workgroup, fewer while that leaves CUs idle
+    const size_t per = std::min(whole_per, std::max<size_t>(2, (n + 255) / 256));
+    for (auto& sp : srcs) push_groups(jobs, sp.first, sp.second, per);
     return;
   }
   int32_t row = prow0;
@@ -546,40 +570,48 @@ void push_level(std::vector<JumpJob>& jobs, std::vector<CombineJob>& comb,
 }
 
 // Levels for windows 1 .. S-1 (s - 1 = 4096 c + 64 a + b; row S holds W_idx;
-// part rows from S + 1): A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a)
-// = C_c(W(1 + 64 a)); B: W(base + b) = B_b(W(base)).
-void build_levels(uint64_t S, std::vector<JumpJob> lv[3], std::vector<CombineJob> cb[3]) {
+// part rows from S + 1) with the jump table of substream length ki:
+// A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a) = C_c(W(1 + 64 a));
+// B: W(base + b) = B_b(W(base)).  Level B is throughput-bound once it has
+// >= 256 jumps (8 whole jumps per workgroup, one table), else split like A, C.
+void build_levels(uint64_t S, int ki, std::vector<JumpJob> lv[3], std::vector<CombineJob> cb[3]) {
   const uint64_t R = kMtJumpRadix;
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
   const int32_t prow0 = static_cast<int32_t>(S + 1);
+  const int32_t t0 = ki * kMtJumpRows;  // the table's first row
   {
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t a = 0; a <= last / R && a < R; ++a)
-      pd.push_back({kMtRowA + static_cast<int32_t>(a), static_cast<int32_t>(1 + R * a)});
-    push_level(lv[0], cb[0], {{static_cast<int32_t>(S), pd}}, prow0);
+      pd.push_back({t0 + kMtRowA + static_cast<int32_t>(a), static_cast<int32_t>(1 + R * a)});
+    push_level(lv[0], cb[0], {{static_cast<int32_t>(S), pd}}, prow0, 2);
   }
   {
     std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>> srcs;
     for (uint64_t a = 0; a < R && R * a <= last; ++a) {  // C: per source W(1 + 64 a), its c digits
       std::vector<std::pair<int32_t, int32_t>> pd;
       for (uint64_t c = 1; c < R && R * R * c + R * a <= last; ++c)
-        pd.push_back({kMtRowC + static_cast<int32_t>(c), static_cast<int32_t>(1 + R * R * c + R * a)});
+        pd.push_back({t0 + kMtRowC + static_cast<int32_t>(c), static_cast<int32_t>(1 + R * R * c + R * a)});
       if (!pd.empty()) srcs.push_back({static_cast<int32_t>(1 + R * a), pd});
     }
-    push_level(lv[1], cb[1], srcs, prow0);
+    push_level(lv[1], cb[1], srcs, prow0, 2);
   }
-  for (uint64_t base = 0; base <= last; base += R) {  // B: per source W(1 + base)
-    std::vector<std::pair<int32_t, int32_t>> pd;
-    for (uint64_t b = 1; b < R && base + b <= last; ++b)
-      pd.push_back({kMtRowB + static_cast<int32_t>(b), static_cast<int32_t>(1 + base + b)});
-    push_groups(lv[2], static_cast<int32_t>(1 + base), pd, kJumpWaves);
+  {
+    std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>> srcs;
+    for (uint64_t base = 0; base <= last; base += R) {  // B: per source W(1 + base)
+      std::vector<std::pair<int32_t, int32_t>> pd;
+      for (uint64_t b = 1; b < R && base + b <= last; ++b)
+        pd.push_back({t0 + kMtRowB + static_cast<int32_t>(b), static_cast<int32_t>(1 + base + b)});
+      if (!pd.empty()) srcs.push_back({static_cast<int32_t>(1 + base), pd});
+    }
+    push_level(lv[2], cb[2], srcs, prow0, kJumpWaves);
   }
 }
 
-// >= the three levels with padding (split levels: jumps x parts <= 512 jobs,
-// 2 per workgroup of 8 -> <= 2048 entries each)
-uint64_t jobs_cap(uint64_t S) { return 2 * S + 4 * 64 * kJumpWaves + 2 * 4 * kPartRows + 1024; }
+// >= the three levels with padding (whole B jumps: 8 per 63-jump source; whole
+// C jumps: 2 per workgroup of 8, < S / 16; split levels: jumps x parts <= 512
+// jobs, 2 per workgroup of 8 -> <= 2048 entries each)
+uint64_t jobs_cap(uint64_t S) { return 2 * S + 3 * 4 * kPartRows + 1024; }
 
 constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
 
@@ -595,6 +627,34 @@ extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
 
 namespace dn {
 namespace {
+
+// Per-thread host side of a draw: the job tables of the last substream count
+// (they depend on S only) and a pinned staging buffer for the small copies
+// (from pageable memory HIP stages every copy through a buffer of its own and
+// the host waits for it).  The buffer is reused only after the previous
+// call's stream synchronize; it is never freed (one per calling thread; at
+// process exit the runtime may be gone before thread-local destructors run).
+struct MtHost {
+  uint64_t S = ~0ull;
+  int ki = -1;
+  std::vector<JumpJob> lv[3];
+  std::vector<CombineJob> cb[3];
+  std::vector<uint32_t> jobs;  // lv then cb, as copied to the device
+  uint32_t* pin = nullptr;
+  size_t pin_words = 0;
+};
+thread_local MtHost tls_mt;
+
+uint32_t* mt_pinned(MtHost& h, size_t words) {
+  if (h.pin_words < words) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, words * 4, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (h.pin) (void)hipHostFree(h.pin);
+    h.pin = static_cast<uint32_t*>(p);
+    h.pin_words = words;
+  }
+  return h.pin;
+}
 
 // The device draw of n_elem * tm1 coefficients from CPython state
 // (mt_state, *mt_index): jump levels, then `launch_gen(ga, S)` (the
@@ -622,50 +682,67 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   uint64_t fpos = 0, ftf = 0;
   if (words > h) {
     const uint64_t m_end = words - h, q = (m_end + kMtN - 1) / kMtN, tf = kMtN * q;
-    uint64_t sg = (tf + kMtN - 1 - static_cast<uint64_t>(idx)) / kMtJumpL;  // idx + sg L - 624 < tf
+    const uint64_t Lk = 17 * mt_sub_draws(mt_sub_len(ncoef));  // words per substream
+    uint64_t sg = (tf + kMtN - 1 - static_cast<uint64_t>(idx)) / Lk;  // idx + sg L - 624 < tf
     if (sg > S - 1) sg = S - 1;
     sig = static_cast<int32_t>(sg);
-    fpos = sg ? static_cast<uint64_t>(idx) + sg * kMtJumpL - kMtN : 0;
+    fpos = sg ? static_cast<uint64_t>(idx) + sg * Lk - kMtN : 0;
     ftf = tf;
     fidx = static_cast<int32_t>(m_end - kMtN * (q - 1));
   }
 
   // scratch: head (flag at 0, final array at 256) | windows 0..S (row 0 the
   // caller's array, row S that array advanced idx words) | part rows (split
-  // levels) | jump jobs | combine jobs.  Two copies: [zeroed head, row 0] and
-  // [jobs, combine jobs]; row S is written by the host between them.
-  std::vector<JumpJob> lv[3];
-  std::vector<CombineJob> cb[3];
-  build_levels(S, lv, cb);
-  const uint64_t njobs = lv[0].size() + lv[1].size() + lv[2].size();
-  const uint64_t ncomb = cb[0].size() + cb[1].size() + cb[2].size();
-  if (njobs > jobs_cap(S) || ncomb > kCombineCap) return set_error(DN_ERR_ARG, "%s: job table overflow", name);
-  std::vector<uint32_t> st1(kHead / 4 + kMtN, 0u);
-  std::memcpy(st1.data() + kHead / 4, mt_state, kMtN * 4);
-  std::vector<uint32_t> st2(kMtN);
-  mt_advance_window(mt_state, static_cast<uint64_t>(idx), st2.data());
-  std::vector<uint32_t> st3((njobs * sizeof(JumpJob) + ncomb * sizeof(CombineJob)) / 4);
-  {
+  // levels) | jump jobs | combine jobs.  Three copies from the pinned
+  // staging buffer [zeroed head, row 0 | row S | jobs]; the head comes back
+  // into its tail.
+  const int ki = mt_sub_len(ncoef);
+  MtHost& H = tls_mt;
+  if (H.S != S || H.ki != ki) {
+    for (auto& l : H.lv) l.clear();
+    for (auto& c : H.cb) c.clear();
+    H.S = ~0ull;
+    build_levels(S, ki, H.lv, H.cb);
+    uint64_t nj = 0, nc = 0;
+    for (auto& l : H.lv) nj += l.size();
+    for (auto& c : H.cb) nc += c.size();
+    if (nj > jobs_cap(S) || nc > kCombineCap) return set_error(DN_ERR_ARG, "%s: job table overflow", name);
+    H.jobs.assign((nj * sizeof(JumpJob) + nc * sizeof(CombineJob)) / 4, 0u);
     uint64_t o = 0;
-    for (auto& l : lv) {
-      std::memcpy(st3.data() + o, l.data(), l.size() * sizeof(JumpJob));
+    for (auto& l : H.lv) {
+      std::memcpy(H.jobs.data() + o, l.data(), l.size() * sizeof(JumpJob));
       o += l.size() * sizeof(JumpJob) / 4;
     }
-    for (auto& c : cb) {
-      std::memcpy(st3.data() + o, c.data(), c.size() * sizeof(CombineJob));
+    for (auto& c : H.cb) {
+      std::memcpy(H.jobs.data() + o, c.data(), c.size() * sizeof(CombineJob));
       o += c.size() * sizeof(CombineJob) / 4;
     }
+    H.S = S;
+    H.ki = ki;
   }
+  const auto& lv = H.lv;
+  const auto& cb = H.cb;
+  const uint64_t njobs = lv[0].size() + lv[1].size() + lv[2].size();
+  const size_t w1 = kHead / 4 + kMtN, w2 = kMtN, w3 = H.jobs.size(), wh = 256 / 4 + kMtN;
+  uint32_t* pin = mt_pinned(H, w1 + w2 + w3 + wh);
+  if (!pin) return set_error(DN_ERR_HIP, "%s: pinned staging buffer", name);
+  uint32_t *st1 = pin, *st2 = pin + w1, *st3 = st2 + w2, *head = st3 + w3;
+  std::memset(st1, 0, kHead);
+  std::memcpy(st1 + kHead / 4, mt_state, kMtN * 4);
+  mt_advance_window(mt_state, static_cast<uint64_t>(idx), st2);
+  if (w3) std::memcpy(st3, H.jobs.data(), w3 * 4);
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
   uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead);
   JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead + (S + 1 + kPartRows) * kMtN * 4);
   CombineJob* dcomb = reinterpret_cast<CombineJob*>(djobs + njobs);
-  hipError_t err = hipMemcpyAsync(sc, st1.data(), st1.size() * 4, hipMemcpyHostToDevice, s);
-  if (err == hipSuccess) err = hipMemcpyAsync(dwin + S * kMtN, st2.data(), st2.size() * 4, hipMemcpyHostToDevice, s);
-  if (err == hipSuccess && !st3.empty())
-    err = hipMemcpyAsync(djobs, st3.data(), st3.size() * 4, hipMemcpyHostToDevice, s);
-  if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
+  hipError_t err = hipMemcpyAsync(sc, st1, w1 * 4, hipMemcpyHostToDevice, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(dwin + S * kMtN, st2, w2 * 4, hipMemcpyHostToDevice, s);
+  if (err == hipSuccess && w3) err = hipMemcpyAsync(djobs, st3, w3 * 4, hipMemcpyHostToDevice, s);
+  if (err != hipSuccess) {
+    (void)hipStreamSynchronize(s);  // the staging buffer is reused by the next call
+    return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
+  }
   uint64_t off = 0, coff = 0;
   for (int k = 0; k < 3; ++k) {
     if (!lv[k].empty()) {
@@ -683,6 +760,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   ga.flag = reinterpret_cast<uint32_t*>(sc);
   ga.fin = reinterpret_cast<uint32_t*>(sc + 256);
   ga.ncoef = ncoef;
+  ga.sub_draws = mt_sub_draws(ki);
   ga.vb = dn_m521_vec_bytes(n_elem);
   ga.tm1_magic = ((1ull << 32) + static_cast<uint64_t>(tm1) - 1) / static_cast<uint64_t>(tm1);
   ga.S = static_cast<uint32_t>(S);
@@ -694,17 +772,20 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   ga.n_elem = n_elem;
   launch_gen(ga, s);
   err = hipGetLastError();
-  if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: launch: %s", name, hipGetErrorString(err));
+  if (err != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    return set_error(DN_ERR_HIP, "%s: launch: %s", name, hipGetErrorString(err));
+  }
 
-  std::vector<uint32_t> head(256 / 4 + kMtN);  // flag .. final array
-  err = hipMemcpyAsync(head.data(), sc, head.size() * 4, hipMemcpyDeviceToHost, s);
-  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  err = hipMemcpyAsync(head, sc, wh * 4, hipMemcpyDeviceToHost, s);  // flag .. final array
+  const hipError_t serr = hipStreamSynchronize(s);
+  if (err == hipSuccess) err = serr;
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   // DN_MT_FORCE_RETRY=1 (tuning build) takes the rejected-draw exit so the
   // caller's host fallback can be exercised.
   const char* fr = tune_env("DN_MT_FORCE_RETRY");
   if (head[0] || (fr && fr[0] == '1')) return set_error(DN_ERR_RETRY, "%s: a draw was rejected; redo on the host", name);
-  if (sig >= 0) std::memcpy(mt_state, head.data() + 256 / 4, kMtN * 4);
+  if (sig >= 0) std::memcpy(mt_state, head + 256 / 4, kMtN * 4);
   *mt_index = fidx;
   return DN_OK;
 }

@@ -330,8 +330,8 @@ def test_tile_map_and_grid_cap_do_not_change_results(N, cap, monkeypatch):
 @pytest.mark.parametrize("n,tm1,pre", [(1, 2, 0), (1000, 2, 3), (40000, 2, 624), (40000, 4, 100),
                                        (100003, 1, 7), (1 << 20, 2, 0), ((1 << 20) + 77, 3, 555)])
 def test_device_mt_draw_equals_host_draw(n, tm1, pre):
-    """dn_mt19937_draw_coeffs_device (jump-ahead substreams of 17*2^16 words,
-    one wave each) gives the host draw's block byte for byte — the reference's
+    """dn_mt19937_draw_coeffs_device (jump-ahead substreams of 17*2^k words,
+    k = 10 / 12 / 14 by size, one wave each) gives the host draw's block byte for byte — the reference's
     randint(1, p-1) sequence — and leaves random.Random in the same state;
     `pre` words drawn first put CPython's index mid-array."""
     a = random.Random(2024 + n)
@@ -343,6 +343,23 @@ def test_device_mt_draw_equals_host_draw(n, tm1, pre):
     got = torch.zeros((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
     assert _native.mt_draw_coeffs_device(b, n, tm1, got)
     assert np.array_equal(got.cpu().numpy(), want)
+    assert a.getstate() == b.getstate()
+
+
+@pytest.mark.parametrize("n,tm1", [((1 << 20) - 3, 2), ((1 << 23) - 5, 2), (1 << 23, 2)])
+def test_device_mt_draw_at_substream_length_boundaries(n, tm1):
+    """The device draw picks its substream length by size (2^10 draws below
+    2^21 coefficients, 2^12 below 2^24, else 2^14): the largest draws of the
+    two short lengths (~2048 / ~4096 substreams, level B with whole jumps) and
+    the first of the long one equal the host draw, same final state."""
+    a = random.Random(n)
+    a.getrandbits(32 * 333)
+    b = random.Random()
+    b.setstate(a.getstate())
+    got = torch.empty((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    assert _native.mt_draw_coeffs_device(b, n, tm1, got)
+    want = torch.from_numpy(_native.mt_draw_coeffs(a, n, tm1)).to(dev())
+    assert torch.equal(got, want)
     assert a.getstate() == b.getstate()
 
 

@@ -138,7 +138,7 @@ def jump(win, g):
     return r
 
 
-def main(out_path):
+def char_poly():
     rs = random.Random(20251016)
     win = list(rs.getstate()[1][:N])
     bits = []
@@ -149,23 +149,28 @@ def main(out_path):
     assert L == DEG, L
     P = int(bin(C)[2:].zfill(L + 1)[::-1], 2)
     assert P.bit_length() - 1 == DEG
+    return P
+
+
+def jump_polys(P, l_words):
+    """[(name, J, x^J mod P)] of the A, C, B rows for substreams of l_words, checked."""
     red = Reducer(P)
     mm = lambda x, y: red(clmul(x, y))  # noqa: E731
-    xL = xpow(L_WORDS, P)
-    x64L = xpow(64 * L_WORDS, P)
-    x4096L = xpow(4096 * L_WORDS, P)
+    xL = xpow(l_words, P)
+    x64L = xpow(64 * l_words, P)
+    x4096L = xpow(4096 * l_words, P)
     polys = []
-    g = xpow(L_WORDS - N, P)
+    g = xpow(l_words - N, P)
     for a in range(RADIX):  # A_a = x^(L - 624 + 64 a L)
-        polys.append((f"A{a}", L_WORDS - N + 64 * a * L_WORDS, g))
+        polys.append((f"A{a}", l_words - N + 64 * a * l_words, g))
         g = mm(g, x64L)
     g = x4096L
     for c in range(1, RADIX):  # C_c = x^(4096 c L)
-        polys.append((f"C{c}", 4096 * c * L_WORDS, g))
+        polys.append((f"C{c}", 4096 * c * l_words, g))
         g = mm(g, x4096L)
     g = xL
     for b in range(1, RADIX):  # B_b = x^(b L)
-        polys.append((f"B{b}", b * L_WORDS, g))
+        polys.append((f"B{b}", b * l_words, g))
         g = mm(g, xL)
     for name, J, gp in polys[::17]:  # products vs direct square-and-multiply
         assert gp == xpow(J, P), name
@@ -177,6 +182,28 @@ def main(out_path):
         for _ in range(J):
             b = step(b)
         assert a[1:] == b[1:] and (a[0] ^ b[0]) >> 31 == 0, name
+    return polys
+
+
+def write_polys(f, macro, polys):
+    nw = (DEG + 1 + 63) // 64
+    f.write(f"#define {macro} {{ \\\n")
+    for name, J, gp in polys:
+        f.write(f"  /* {name}: J = {J} */ {{ \\")
+        ws = [(gp >> (64 * i)) & ((1 << 64) - 1) for i in range(nw)]
+        for i, wv in enumerate(ws):
+            if i % 6 == 0:
+                f.write("\n   ")
+            f.write(f" 0x{wv:016x}ull,")
+            if i % 6 == 5 or i == nw - 1:
+                f.write(" \\")
+        f.write("\n  }, \\\n")
+    f.write("}\n")
+
+
+def main(out_path):
+    P = char_poly()
+    polys = jump_polys(P, L_WORDS)
     nw = (DEG + 1 + 63) // 64
     with open(out_path, "w") as f:
         f.write("// Generated by tools/gen_mt_jump.py — do not edit.\n")
@@ -191,21 +218,30 @@ def main(out_path):
         f.write("constexpr int kMtRowA = 0, kMtRowC = 63, kMtRowB = 126;\n")
         f.write(f"constexpr int kMtJumpRows = {len(polys)};\n")
         f.write("// initializer of a [kMtJumpRows][kMtPolyWords] uint64_t array (host and device copies)\n")
-        f.write("#define DN_MT_JUMP_POLYS { \\\n")
-        for name, J, gp in polys:
-            f.write(f"  /* {name}: J = {J} */ {{ \\")
-            ws = [(gp >> (64 * i)) & ((1 << 64) - 1) for i in range(nw)]
-            for i, wv in enumerate(ws):
-                if i % 6 == 0:
-                    f.write("\n   ")
-                f.write(f" 0x{wv:016x}ull,")
-                if i % 6 == 5 or i == nw - 1:
-                    f.write(" \\")
-            f.write("\n  }, \\\n")
-        f.write("}\n")
+        write_polys(f, "DN_MT_JUMP_POLYS", polys)
+    print("wrote", out_path)
+
+
+def main_short(out_path):
+    """The same rows for shorter substreams (17 * 2^10 and 17 * 2^12 words:
+    2^10 / 2^12 whole draws), which the device draw uses for smaller vectors
+    so that a substream's sequential generation does not dominate."""
+    P = char_poly()
+    with open(out_path, "w") as f:
+        f.write("// Generated by tools/gen_mt_jump.py --short — do not edit.\n")
+        f.write("// As mt19937_jump.inc (same rows A, C, B and layout) for substreams of\n")
+        f.write("// L = 17 * 2^10 and 17 * 2^12 words.\n")
+        for k in (10, 12):
+            lw = 17 * (1 << k)
+            f.write(f"constexpr uint64_t kMtJumpL{k} = {lw}ull;\n")
+            write_polys(f, f"DN_MT_JUMP_POLYS_L{k}", jump_polys(P, lw))
     print("wrote", out_path)
 
 
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "delta-node_amd", "csrc", "mt19937_jump.inc"))
+    csrc = os.path.join(root, "delta-node_amd", "csrc")
+    if len(sys.argv) > 1 and sys.argv[1] == "--short":
+        main_short(sys.argv[2] if len(sys.argv) > 2 else os.path.join(csrc, "mt19937_jump_short.inc"))
+    else:
+        main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(csrc, "mt19937_jump.inc"))
