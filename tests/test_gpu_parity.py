@@ -476,3 +476,37 @@ def test_device_mt_draw_shard_equals_slice_of_full_draw(N, lo, hi):
     assert np.array_equal(block_limbs(blk, hi - lo), block_limbs(want.contiguous(), hi - lo))
     assert ss_shard.random.getstate() == ss_full.random.getstate()
     assert not ss_shard.last_draw_rejected
+
+
+def test_fused_draw_split_from_concurrent_threads():
+    """make_shares_vec's fused draw keeps per-call host state per thread (job
+    tables, pinned staging): four threads, each with its own SecretShare and
+    sizes that pick different substream lengths, give the same shares and the
+    same final random states as the calls made one after another."""
+    import threading
+
+    sizes = [5000, 1 << 18, (1 << 20) + 9, 70001]
+    sec = torch.from_numpy(secrets_int64(99, max(sizes))).to(dev())
+
+    def run(i, out, states):
+        ss = shamir.SecretShare(3)
+        ss.random.seed(1000 + i)
+        res = []
+        for _ in range(3):
+            res.append(ss.make_shares_vec(sec[: sizes[i]], 5).clone())
+        torch.cuda.synchronize()
+        out[i] = res
+        states[i] = ss.random.getstate()
+
+    seq, seq_st = {}, {}
+    for i in range(len(sizes)):
+        run(i, seq, seq_st)
+    par, par_st = {}, {}
+    ths = [threading.Thread(target=run, args=(i, par, par_st)) for i in range(len(sizes))]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    for i in range(len(sizes)):
+        assert par_st[i] == seq_st[i]
+        assert all(torch.equal(a, b) for a, b in zip(par[i], seq[i]))
