@@ -161,7 +161,7 @@ constexpr int kEVWords = 64 * 2;                      // words per chunk value v
 constexpr int kEPair = 16 * kEVWords + 2;              // 2050 words
 constexpr int kEWrap = ((5 * kEPair + 63) / 64) * 64;  // 10304 words
 constexpr int kEWords = kEWrap + 5 * kEPair;           // 82 KB
-constexpr int kJumpWaves = 8;  // jumps (waves) per workgroup, all from one source
+constexpr int kJumpWaves = 16;  // at most this many jumps (waves) per workgroup, all from one source and part
 
 // a ^ b ^ c in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96;
 // hipcc keeps two v_xor_b32 otherwise)
@@ -227,11 +227,12 @@ __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, cons
 //     register, its operands gathered by 3 ds_bpermute;
 //   * the XOR of 16 table windows into the 624 window words (10 registers;
 //     80 ds_read_b64 and 80 v_bitop3 per lane).
-__global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs a) {
+template <int W>  // waves per workgroup (8 or 16)
+__global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t E[kEWords];
   __shared__ uint32_t ext[kMtN + 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  const uint32_t j0 = blockIdx.x * kJumpWaves;
+  const uint32_t j0 = blockIdx.x * W;
   const JumpJob* jp = a.jobs + __builtin_amdgcn_readfirstlane(j0 + wid < a.njobs ? j0 + wid : j0);
   const int32_t poly = __builtin_amdgcn_readfirstlane(jp->poly), dsti = __builtin_amdgcn_readfirstlane(jp->dst);
   // the workgroup's jobs share the source and lo (one table; job j0 is never padding)
@@ -240,7 +241,7 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
   const uint32_t* src = a.wins + static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(a.jobs[j0].src)) * kMtN;
   if (lo == 0) {
     // the source stream: words 0..623 of W, then 63 more (each from words <= 459 of W)
-    for (uint32_t i = tid; i < kMtN; i += 64u * kJumpWaves) ext[i] = src[i];
+    for (uint32_t i = tid; i < kMtN; i += 64u * W) ext[i] = src[i];
     __syncthreads();
     if (tid < 63u) ext[kMtN + tid] = mt_mix(ext[tid], ext[tid + 1], ext[tid + kMtM]);
     __syncthreads();
@@ -250,7 +251,7 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
     // 624 + i needs words i, i + 1, i + 397).  A step writes ring slots
     // 624..850 past its base and reads 0..623, so one barrier per step.
     uint32_t* ring = E;
-    for (uint32_t i = tid; i < kMtN; i += 64u * kJumpWaves) ring[i] = src[i];
+    for (uint32_t i = tid; i < kMtN; i += 64u * W) ring[i] = src[i];
     __syncthreads();
     const uint32_t need = 64u * static_cast<uint32_t>(lo) + 687u;
     for (uint32_t base = 0; base + kMtN < need; base += kMtN - kMtM) {
@@ -260,10 +261,10 @@ __global__ void __launch_bounds__(64 * kJumpWaves) mt_jump_kernel(const JumpArgs
       }
       __syncthreads();
     }
-    for (uint32_t i = tid; i < 687u; i += 64u * kJumpWaves) ext[i] = ring[(64u * static_cast<uint32_t>(lo) + i) & 1023u];
+    for (uint32_t i = tid; i < 687u; i += 64u * W) ext[i] = ring[(64u * static_cast<uint32_t>(lo) + i) & 1023u];
     __syncthreads();
   }
-  for (uint32_t e = tid; e < static_cast<uint32_t>(kEWords); e += 64u * kJumpWaves) {
+  for (uint32_t e = tid; e < static_cast<uint32_t>(kEWords); e += 64u * W) {
     const uint32_t wrap = e >= static_cast<uint32_t>(kEWrap) ? 1u : 0u, re = e - wrap * kEWrap;
     const uint32_t i = re / kEPair, rem = re - i * kEPair;  // pair plane, position in it
     const uint32_t v = rem / kEVWords, mw = rem - v * kEVWords, m = mw >> 1;
@@ -513,46 +514,54 @@ uint64_t mt_subs(uint64_t ncoef) {
 
 constexpr int32_t kFullSpan = kMtPolyWords << 16;  // words [0, 312)
 constexpr int kMaxParts = 16;
-constexpr uint64_t kPartRows = 512;  // part windows of one split level (jobs x parts <= 512)
-constexpr uint64_t kCombineCap = 64 + 256 + 256;  // split jumps of levels A, C and B
+constexpr uint64_t kPartRows = 4096;  // part windows of one split level (jumps x parts <= 4096)
 
-// Jump jobs of one level, grouped by source window (and part) in workgroups
-// of kJumpWaves jobs (padding: dst -1).
-void push_group(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd,
-                int32_t span) {
-  for (size_t i = 0; i < pd.size(); ++i) jobs.push_back({src, pd[i].first, pd[i].second, span});
-  while (jobs.size() % kJumpWaves) jobs.push_back({src, 0, -1, span});
+// The jobs of one level: W waves per workgroup (one job each; padding jobs
+// have dst -1), grouped by source window and part (one table per workgroup).
+struct Level {
+  int W = 8;
+  std::vector<JumpJob> jobs;
+  std::vector<CombineJob> comb;
+};
+
+void push_group(Level& L, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd, int32_t span) {
+  for (size_t i = 0; i < pd.size(); ++i) L.jobs.push_back({src, pd[i].first, pd[i].second, span});
+  while (L.jobs.size() % static_cast<size_t>(L.W)) L.jobs.push_back({src, 0, -1, span});
 }
 
-// split a source's jobs into groups of at most `per` (fewer jumps per
-// workgroup = less LDS traffic per CU: a latency-bound level)
-void push_groups(std::vector<JumpJob>& jobs, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd,
-                 size_t per, int32_t span = kFullSpan) {
+// a source's jobs in groups of at most `per`
+void push_groups(Level& L, int32_t src, const std::vector<std::pair<int32_t, int32_t>>& pd, size_t per,
+                 int32_t span = kFullSpan) {
   for (size_t i = 0; i < pd.size(); i += per)
-    push_group(jobs, src, std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + per)),
+    push_group(L, src, std::vector<std::pair<int32_t, int32_t>>(pd.begin() + i, pd.begin() + std::min(pd.size(), i + per)),
                span);
 }
 
-// One latency-bound level: (source, [(poly, dst)]) lists.  Few jumps (< 256)
-// are split into P parts (jumps x P <= 512, workgroups of 2 jobs: every CU
-// busy, ~312 / P Horner steps each) written to part rows prow0 .. and XORed
-// into their windows by `comb`; otherwise `whole_per` whole jumps per workgroup.
-void push_level(std::vector<JumpJob>& jobs, std::vector<CombineJob>& comb,
-                const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs, int32_t prow0,
-                size_t whole_per) {
-  size_t n = 0;
-  for (auto& sp : srcs) n += sp.second.size();
-  const int P = n == 0 || n >= 256 ? 1 : static_cast<int>(std::min<size_t>(kMaxParts, kPartRows / n));
+// One level: (source, [(poly, dst)]) lists of n jumps in all.  A jump's
+// Horner chain is ~312 dependent steps of LDS-table reads, so the level is
+// latency-bound unless every CU holds many waves.  The level therefore splits
+// each jump into P = min(16, 4096 / n) parts over word ranges of g (n P part
+// jobs, each ~312 / P steps, written to part rows prow0 .. and XORed into the
+// jump's window by mt_combine_kernel) and groups per = clamp(n P / 256, 2,
+// 16) part jobs of one source and part per workgroup (one table): ~256
+// workgroups, one per CU (82 KB of LDS each), 2..16 waves.  Large levels
+// (n >= 4096) stay whole, 16 jumps per workgroup.
+void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs,
+                int32_t prow0) {
+  size_t n = 0, most = 0;  // jumps, and the most of one source
+  for (auto& sp : srcs) n += sp.second.size(), most = std::max(most, sp.second.size());
+  if (n == 0) return;
+  const int P = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kMaxParts, kPartRows / n)));
+  const size_t per = std::min<size_t>(kJumpWaves, std::max<size_t>(2, (n * P + 255) / 256));
+  L.W = std::min(per, most) > 8 ? 16 : 8;
   if (P == 1) {
-    // whole jumps: at most whole_per per workgroup, fewer while that leaves CUs idle
-    const size_t per = std::min(whole_per, std::max<size_t>(2, (n + 255) / 256));
-    for (auto& sp : srcs) push_groups(jobs, sp.first, sp.second, per);
+    for (auto& sp : srcs) push_groups(L, sp.first, sp.second, per);
     return;
   }
   int32_t row = prow0;
   for (auto& sp : srcs)
     for (auto& pd : sp.second) {
-      comb.push_back({pd.second, row, P, 0});
+      L.comb.push_back({pd.second, row, P, 0});
       row += P;
     }
   for (int j = 0; j < P; ++j) {
@@ -564,7 +573,7 @@ void push_level(std::vector<JumpJob>& jobs, std::vector<CombineJob>& comb,
         pd.push_back({q.first, row});
         row += P;
       }
-      push_groups(jobs, sp.first, pd, 2, lo | hi << 16);
+      push_groups(L, sp.first, pd, per, lo | hi << 16);
     }
   }
 }
@@ -572,9 +581,8 @@ void push_level(std::vector<JumpJob>& jobs, std::vector<CombineJob>& comb,
 // Levels for windows 1 .. S-1 (s - 1 = 4096 c + 64 a + b; row S holds W_idx;
 // part rows from S + 1) with the jump table of substream length ki:
 // A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a) = C_c(W(1 + 64 a));
-// B: W(base + b) = B_b(W(base)).  Level B is throughput-bound once it has
-// >= 256 jumps (8 whole jumps per workgroup, one table), else split like A, C.
-void build_levels(uint64_t S, int ki, std::vector<JumpJob> lv[3], std::vector<CombineJob> cb[3]) {
+// B: W(base + b) = B_b(W(base)).
+void build_levels(uint64_t S, int ki, Level lv[3]) {
   const uint64_t R = kMtJumpRadix;
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
@@ -584,7 +592,7 @@ void build_levels(uint64_t S, int ki, std::vector<JumpJob> lv[3], std::vector<Co
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t a = 0; a <= last / R && a < R; ++a)
       pd.push_back({t0 + kMtRowA + static_cast<int32_t>(a), static_cast<int32_t>(1 + R * a)});
-    push_level(lv[0], cb[0], {{static_cast<int32_t>(S), pd}}, prow0, 2);
+    push_level(lv[0], {{static_cast<int32_t>(S), pd}}, prow0);
   }
   {
     std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>> srcs;
@@ -594,7 +602,7 @@ void build_levels(uint64_t S, int ki, std::vector<JumpJob> lv[3], std::vector<Co
         pd.push_back({t0 + kMtRowC + static_cast<int32_t>(c), static_cast<int32_t>(1 + R * R * c + R * a)});
       if (!pd.empty()) srcs.push_back({static_cast<int32_t>(1 + R * a), pd});
     }
-    push_level(lv[1], cb[1], srcs, prow0, 2);
+    push_level(lv[1], srcs, prow0);
   }
   {
     std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>> srcs;
@@ -604,46 +612,49 @@ void build_levels(uint64_t S, int ki, std::vector<JumpJob> lv[3], std::vector<Co
         pd.push_back({t0 + kMtRowB + static_cast<int32_t>(b), static_cast<int32_t>(1 + base + b)});
       if (!pd.empty()) srcs.push_back({static_cast<int32_t>(1 + base), pd});
     }
-    push_level(lv[2], cb[2], srcs, prow0, kJumpWaves);
+    push_level(lv[2], srcs, prow0);
   }
 }
 
-// >= the three levels with padding (whole B jumps: 8 per 63-jump source; whole
-// C jumps: 2 per workgroup of 8, < S / 16; split levels: jumps x parts <= 512
-// jobs, 2 per workgroup of 8 -> <= 2048 entries each)
-uint64_t jobs_cap(uint64_t S) { return 2 * S + 3 * 4 * kPartRows + 1024; }
-
-constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
-
-}  // namespace
-}  // namespace dn
-
-using namespace dn;
-
-extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
-  const uint64_t S = tm1 > 0 ? mt_subs(n_elem * static_cast<uint64_t>(tm1)) : 0;
-  return kHead + (S + 1 + kPartRows) * kMtN * 4 + jobs_cap(S) * sizeof(JumpJob) + kCombineCap * sizeof(CombineJob);
-}
-
-namespace dn {
-namespace {
-
 // Per-thread host side of a draw: the job tables of the last substream count
-// (they depend on S only) and a pinned staging buffer for the small copies
-// (from pageable memory HIP stages every copy through a buffer of its own and
-// the host waits for it).  The buffer is reused only after the previous
-// call's stream synchronize; it is never freed (one per calling thread; at
-// process exit the runtime may be gone before thread-local destructors run).
+// and length (they depend on S and ki only) and a pinned staging buffer for
+// the small copies (from pageable memory HIP stages every copy through a
+// buffer of its own and the host waits for it).  The buffer is reused only
+// after the previous call's stream synchronize; it is never freed (one per
+// calling thread; at process exit the runtime may be gone before
+// thread-local destructors run).
 struct MtHost {
   uint64_t S = ~0ull;
   int ki = -1;
-  std::vector<JumpJob> lv[3];
-  std::vector<CombineJob> cb[3];
-  std::vector<uint32_t> jobs;  // lv then cb, as copied to the device
+  Level lv[3];
+  std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint32_t* pin = nullptr;
   size_t pin_words = 0;
 };
 thread_local MtHost tls_mt;
+
+MtHost& mt_levels(uint64_t S, int ki) {
+  MtHost& H = tls_mt;
+  if (H.S != S || H.ki != ki) {
+    for (auto& l : H.lv) l = Level();
+    build_levels(S, ki, H.lv);
+    uint64_t nj = 0, nc = 0;
+    for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
+    H.jobs.assign((nj * sizeof(JumpJob) + nc * sizeof(CombineJob)) / 4, 0u);
+    uint64_t o = 0;
+    for (auto& l : H.lv) {
+      std::memcpy(H.jobs.data() + o, l.jobs.data(), l.jobs.size() * sizeof(JumpJob));
+      o += l.jobs.size() * sizeof(JumpJob) / 4;
+    }
+    for (auto& l : H.lv) {
+      std::memcpy(H.jobs.data() + o, l.comb.data(), l.comb.size() * sizeof(CombineJob));
+      o += l.comb.size() * sizeof(CombineJob) / 4;
+    }
+    H.S = S;
+    H.ki = ki;
+  }
+  return H;
+}
 
 uint32_t* mt_pinned(MtHost& h, size_t words) {
   if (h.pin_words < words) {
@@ -655,6 +666,22 @@ uint32_t* mt_pinned(MtHost& h, size_t words) {
   }
   return h.pin;
 }
+
+constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
+
+}  // namespace
+}  // namespace dn
+
+using namespace dn;
+
+extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
+  const uint64_t ncoef = tm1 > 0 ? n_elem * static_cast<uint64_t>(tm1) : 0;
+  const uint64_t S = ncoef ? mt_subs(ncoef) : 0;
+  return kHead + (S + 1 + kPartRows) * kMtN * 4 + (S ? mt_levels(S, mt_sub_len(ncoef)).jobs.size() * 4 : 0);
+}
+
+namespace dn {
+namespace {
 
 // The device draw of n_elem * tm1 coefficients from CPython state
 // (mt_state, *mt_index): jump levels, then `launch_gen(ga, S)` (the
@@ -697,32 +724,9 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   // staging buffer [zeroed head, row 0 | row S | jobs]; the head comes back
   // into its tail.
   const int ki = mt_sub_len(ncoef);
-  MtHost& H = tls_mt;
-  if (H.S != S || H.ki != ki) {
-    for (auto& l : H.lv) l.clear();
-    for (auto& c : H.cb) c.clear();
-    H.S = ~0ull;
-    build_levels(S, ki, H.lv, H.cb);
-    uint64_t nj = 0, nc = 0;
-    for (auto& l : H.lv) nj += l.size();
-    for (auto& c : H.cb) nc += c.size();
-    if (nj > jobs_cap(S) || nc > kCombineCap) return set_error(DN_ERR_ARG, "%s: job table overflow", name);
-    H.jobs.assign((nj * sizeof(JumpJob) + nc * sizeof(CombineJob)) / 4, 0u);
-    uint64_t o = 0;
-    for (auto& l : H.lv) {
-      std::memcpy(H.jobs.data() + o, l.data(), l.size() * sizeof(JumpJob));
-      o += l.size() * sizeof(JumpJob) / 4;
-    }
-    for (auto& c : H.cb) {
-      std::memcpy(H.jobs.data() + o, c.data(), c.size() * sizeof(CombineJob));
-      o += c.size() * sizeof(CombineJob) / 4;
-    }
-    H.S = S;
-    H.ki = ki;
-  }
-  const auto& lv = H.lv;
-  const auto& cb = H.cb;
-  const uint64_t njobs = lv[0].size() + lv[1].size() + lv[2].size();
+  MtHost& H = mt_levels(S, ki);
+  const Level* lv = H.lv;
+  const uint64_t njobs = lv[0].jobs.size() + lv[1].jobs.size() + lv[2].jobs.size();
   const size_t w1 = kHead / 4 + kMtN, w2 = kMtN, w3 = H.jobs.size(), wh = 256 / 4 + kMtN;
   uint32_t* pin = mt_pinned(H, w1 + w2 + w3 + wh);
   if (!pin) return set_error(DN_ERR_HIP, "%s: pinned staging buffer", name);
@@ -745,15 +749,18 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   }
   uint64_t off = 0, coff = 0;
   for (int k = 0; k < 3; ++k) {
-    if (!lv[k].empty()) {
-      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(lv[k].size())};
-      hipLaunchKernelGGL(mt_jump_kernel, dim3(static_cast<uint32_t>(lv[k].size() / kJumpWaves)), dim3(64 * kJumpWaves),
-                         0, s, ja);
+    const Level& l = lv[k];
+    if (!l.jobs.empty()) {
+      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.jobs.size())};
+      const dim3 grid(static_cast<uint32_t>(l.jobs.size() / static_cast<size_t>(l.W)));
+      if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, s, ja);
+      else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, s, ja);
     }
-    if (!cb[k].empty())
-      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(cb[k].size())), dim3(256), 0, s, dwin, dcomb + coff);
-    off += lv[k].size();
-    coff += cb[k].size();
+    if (!l.comb.empty())
+      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(l.comb.size())), dim3(256), 0, s, dwin,
+                         dcomb + coff);
+    off += l.jobs.size();
+    coff += l.comb.size();
   }
   GenArgs ga{};
   ga.wins = dwin;

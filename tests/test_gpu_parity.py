@@ -492,8 +492,9 @@ def test_fused_draw_split_from_concurrent_threads():
         ss = shamir.SecretShare(3)
         ss.random.seed(1000 + i)
         res = []
-        for _ in range(3):
-            res.append(ss.make_shares_vec(sec[: sizes[i]], 5).clone())
+        for _ in range(3):  # zeroed outputs: the split leaves the last tile's padding alone
+            blk = torch.zeros((5, field.vec_bytes(sizes[i])), dtype=torch.uint8, device=dev())
+            res.append(ss.make_shares_vec(sec[: sizes[i]], 5, out=blk))
         torch.cuda.synchronize()
         out[i] = res
         states[i] = ss.random.getstate()
