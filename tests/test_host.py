@@ -296,3 +296,26 @@ def test_mt19937_skip_third_digit_composes():
             _native.mt_skip(b, first)
             _native.mt_skip(b, total - first)
             assert a.getstate() == b.getstate(), (start, total, first)
+
+
+def test_mt_jump_job_builder_invariants(tmp_path):
+    """The device MT draw's jump-job builder (host code in
+    csrc/mt19937_device.hip), compiled for the host by tools/mt_levels_check.hip:
+    every substream window produced exactly once, sources ready before their
+    level, one table per workgroup, part rows in bounds and covering the
+    polynomial in order — S up to 300 and boundary sizes to 65537, all three
+    substream lengths."""
+    import shutil
+    import subprocess
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "mt_levels_check")
+    subprocess.run([hipcc, "-O1", "-std=c++17", "--offload-arch=gfx950", "-I" + os.path.join(root, "include"),
+                    "-I" + os.path.join(root, "delta-node_amd", "csrc"),
+                    os.path.join(root, "tools", "mt_levels_check.hip"), "-o", exe], check=True, capture_output=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:]
+    assert "fails 0" in r.stdout
