@@ -717,7 +717,7 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
         m = 1 << lg
         ss = shamir.SecretShare(3)
         ss.random.seed(lg)
-        sm, om = sec[:m], out[:, : field.vec_bytes(m)]
+        sm = sec[:m]
         o2 = torch.empty((5, field.vec_bytes(m)), dtype=torch.uint8, device=dev)
         for _ in range(2):
             ss.make_shares_vec(sm, 5, out=o2)
@@ -727,7 +727,7 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
             ss.make_shares_vec(sm, 5, out=o2)
         torch.cuda.synchronize()
         by_size[f"2^{lg}"] = (time.perf_counter() - t0) / 10 * 1e3
-        del om, o2
+        del o2
     return {"workload": f"make_shares_vec(2^{log2n} int64, 5) on SecretShare(3), coefficients = the reference's "
                         "MT19937 draws (shamir.py:59-61), bit-exact", "unit": "elements/s",
             "fused_ms": fm * 1e3, "fused_elems_per_s": n / fm, "draw_then_split_ms": um * 1e3,
