@@ -218,8 +218,9 @@ __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, cons
    ...);
 }
 
-// One workgroup = up to 8 jumps from the same source window W (the host
-// groups them; padding jobs have dst < 0).  Horner over 4-bit chunks of g,
+// One workgroup = up to W jumps (or parts of jumps, words [lo, hi) of g)
+// from the same source window W and the same lo (the host groups them;
+// padding jobs have dst < 0).  Horner over 4-bit chunks of g,
 // 16 chunks (one 64-bit word of g) per step: r <- f^64(r) ^ sum_t
 // f^(4 (15 - t))(T[c_t]); f^m(T[v]) is the window at offset m of T[v]'s own
 // stream, which the workgroup tables once (E, 82 KB of LDS), so a step is
