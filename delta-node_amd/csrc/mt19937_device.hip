@@ -162,6 +162,7 @@ constexpr int kEPair = 16 * kEVWords + 2;              // 2050 words
 constexpr int kEWrap = ((5 * kEPair + 63) / 64) * 64;  // 10304 words
 constexpr int kEWords = kEWrap + 5 * kEPair;           // 82 KB
 constexpr int kJumpWaves = 16;  // at most this many jumps (waves) per workgroup, all from one source and part
+constexpr int kMaxParts = 16;   // at most this many parts per jump
 
 // a ^ b ^ c in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96;
 // hipcc keeps two v_xor_b32 otherwise)
@@ -311,14 +312,18 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   }
 }
 
-// The parts of a split level XORed into their jumps' windows.
-__global__ void __launch_bounds__(256) mt_combine_kernel(uint32_t* wins, const CombineJob* cj) {
+// The parts of a split level XORed into their jumps' windows: one thread per
+// window word, the (at most 16) part loads issued together.
+__global__ void __launch_bounds__(640) mt_combine_kernel(uint32_t* wins, const CombineJob* cj) {
   const CombineJob c = cj[blockIdx.x];
-  for (uint32_t i = threadIdx.x; i < static_cast<uint32_t>(kMtN); i += 256u) {
-    uint32_t x = 0u;
-    for (int32_t j = 0; j < c.parts; ++j) x ^= wins[static_cast<uint64_t>(c.first + j) * kMtN + i];
-    wins[static_cast<uint64_t>(c.dst) * kMtN + i] = x;
-  }
+  const uint32_t i = threadIdx.x;
+  if (i >= static_cast<uint32_t>(kMtN)) return;
+  const uint32_t* p = wins + static_cast<uint64_t>(c.first) * kMtN + i;
+  uint32_t x = 0u;
+#pragma unroll
+  for (int32_t j = 0; j < kMaxParts; ++j)
+    if (j < c.parts) x ^= p[static_cast<uint64_t>(j) * kMtN];
+  wins[static_cast<uint64_t>(c.dst) * kMtN + i] = x;
 }
 
 // ------------------------------------------------------------------ generation
@@ -514,7 +519,6 @@ uint64_t mt_subs(uint64_t ncoef) {
 }
 
 constexpr int32_t kFullSpan = kMtPolyWords << 16;  // words [0, 312)
-constexpr int kMaxParts = 16;
 constexpr uint64_t kPartRows = 4096;  // part windows of one split level (jumps x parts <= 4096)
 
 // The jobs of one level: W waves per workgroup (one job each; padding jobs
@@ -758,7 +762,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
       else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, s, ja);
     }
     if (!l.comb.empty())
-      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(l.comb.size())), dim3(256), 0, s, dwin,
+      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(l.comb.size())), dim3(640), 0, s, dwin,
                          dcomb + coff);
     off += l.jobs.size();
     coff += l.comb.size();
