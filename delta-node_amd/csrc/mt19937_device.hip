@@ -633,6 +633,7 @@ struct MtHost {
   int ki = -1;
   Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
+  uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
   uint32_t* pin = nullptr;
   size_t pin_words = 0;
 };
@@ -645,6 +646,9 @@ MtHost& mt_levels(uint64_t S, int ki) {
     build_levels(S, ki, H.lv);
     uint64_t nj = 0, nc = 0;
     for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
+    H.part_rows = 0;
+    for (auto& l : H.lv)
+      for (auto& c : l.comb) H.part_rows = std::max<uint64_t>(H.part_rows, c.first + c.parts - (S + 1));
     H.jobs.assign((nj * sizeof(JumpJob) + nc * sizeof(CombineJob)) / 4, 0u);
     uint64_t o = 0;
     for (auto& l : H.lv) {
@@ -682,7 +686,9 @@ using namespace dn;
 extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
   const uint64_t ncoef = tm1 > 0 ? n_elem * static_cast<uint64_t>(tm1) : 0;
   const uint64_t S = ncoef ? mt_subs(ncoef) : 0;
-  return kHead + (S + 1 + kPartRows) * kMtN * 4 + (S ? mt_levels(S, mt_sub_len(ncoef)).jobs.size() * 4 : 0);
+  if (!S) return kHead + kMtN * 4;
+  const MtHost& H = mt_levels(S, mt_sub_len(ncoef));
+  return kHead + (S + 1 + H.part_rows) * kMtN * 4 + H.jobs.size() * 4;
 }
 
 namespace dn {
@@ -743,7 +749,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
   uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead);
-  JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead + (S + 1 + kPartRows) * kMtN * 4);
+  JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead + (S + 1 + H.part_rows) * kMtN * 4);
   CombineJob* dcomb = reinterpret_cast<CombineJob*>(djobs + njobs);
   hipError_t err = hipMemcpyAsync(sc, st1, w1 * 4, hipMemcpyHostToDevice, s);
   if (err == hipSuccess) err = hipMemcpyAsync(dwin + S * kMtN, st2, w2 * 4, hipMemcpyHostToDevice, s);
