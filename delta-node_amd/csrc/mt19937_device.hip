@@ -409,10 +409,28 @@ __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb,
   if (e >= a.n_elem) return;
   uint32_t c[T][kLimbs];
   const uint32_t* w = rb + 17u * TM1 * lane;
+  if constexpr (TM1 % 2 == 0) {
+    // an element's 17 (t-1) words start at an even word: 8-B reads, and with
+    // a lane stride of 34 words (t = 3) the 32 lanes of a b64 group hit 32
+    // distinct bank pairs (b32 reads at that stride are 2-way conflicted)
+    uint32_t ww[17 * TM1];
+#pragma unroll
+    for (int k = 0; k < 17 * TM1 / 2; ++k) {
+      const u32x2_t d = *reinterpret_cast<const u32x2_t*>(w + 2 * k);
+      ww[2 * k] = d.x, ww[2 * k + 1] = d.y;
+    }
+#pragma unroll
+    for (int j = 1; j < T; ++j)
+#pragma unroll
+      for (int i = 0; i < kLimbs; ++i) c[j][i] = ww[17 * (j - 1) + i];
+  } else {
+#pragma unroll
+    for (int j = 1; j < T; ++j)
+#pragma unroll
+      for (int i = 0; i < kLimbs; ++i) c[j][i] = w[17 * (j - 1) + i];
+  }
 #pragma unroll
   for (int j = 1; j < T; ++j) {
-#pragma unroll
-    for (int i = 0; i < kLimbs; ++i) c[j][i] = w[17 * (j - 1) + i];
     c[j][16] >>= 23;
     uint32_t all = c[j][1];
 #pragma unroll
@@ -453,7 +471,7 @@ __device__ __forceinline__ void final_run(uint32_t (&Q)[11], const Lanes& L, uin
 // substream's elements (groups of 64 elements) with them as they are drawn.
 template <int T>
 __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
-  extern __shared__ uint32_t s_ring[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t sub = blockIdx.x;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
