@@ -5,10 +5,16 @@ GF(2^521 - 1) of one 2^24-element int64 vector (BASELINE.json `metric`, configs 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`python bench.py --gpus N` with N > 1 and no launcher environment starts
+`torch.distributed.run` with N ranks as a child process and relays rank 0's
+line; under a launcher, --gpus must equal WORLD_SIZE.
+
 One step = `dn_m521_split_u64` (t=3, n=5) over the rank's N elements, then
 `dn_m521_reconstruct` of shares xs (default 1,3,5) back to int64, inputs
 resident in HBM before the timed region (secrets + MT19937 coefficients drawn
-exactly as the reference's `make_shares` would draw them).  Strong scaling, as
+exactly as the reference's `make_shares` would draw them).  The steps rotate
+over --placements separately allocated share buffers, and the line reports
+the split's rate per buffer (`roofline.placement`).  Strong scaling, as
 the metric names it: ONE 2^24-element vector, rank r splitting its tile-aligned
 shard (dist.shard_range); value = 2^24 / max-over-ranks time per step.  At
 N > 1 the line also carries `weak_scaling` (2^24 elements per GPU).
@@ -782,9 +788,58 @@ def load_traffic(path: str):
         return None
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launcher_cmd(gpus: int, argv, port: int) -> list:
+    """The command `bench.py --gpus N` (N > 1, not already under a launcher)
+    runs as a CHILD process: one rank per GPU of this node, rendezvous on
+    127.0.0.1, every rank running this file with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """Run N ranks through torch.distributed.run as a child (never exec: this
+    process has made no GPU call and makes none), pass its output through,
+    and print rank 0's JSON line as the one line on stdout.  Returns the
+    child's exit code."""
+    import subprocess
+
+    backend = os.environ.get("DN_DIST_BACKEND", "nccl")
+    visible = torch.cuda.device_count()  # counts devices without initialising HIP
+    if backend == "nccl" and gpus > visible:
+        print(f"bench.py: --gpus {gpus} with RCCL needs {gpus} visible GPUs, this node has {visible} "
+              "(DN_DIST_BACKEND=gloo rehearses the ranks on fewer GPUs)", file=sys.stderr)
+        return 2
+    proc = subprocess.Popen(launcher_cmd(gpus, argv, free_port()), stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for ln in proc.stdout:
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            line = s
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if line:
+        print(line, flush=True)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) on this node; without a launcher's WORLD_SIZE, N > 1 starts "
+                         "torch.distributed.run with N ranks as a child process")
+    ap.add_argument("--placements", type=int, default=5,
+                    help="share buffers the timed steps rotate over (separate allocations: the split's rate "
+                         "depends on the physical pages of its share buffer, DESIGN.md §5.1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=24, help="elements of the vector = 2^log2n (sharded over the ranks)")
@@ -803,7 +858,14 @@ def main():
                                                             "loopback HTTP to a second process; N=1 only)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ:
+        if (args.gpus or 1) > 1:
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -852,32 +914,40 @@ def main():
         coeffs = sdist.draw_coeffs_sharded(ss, N_total, dev)[:, :vb].contiguous()
     else:
         coeffs = ss.draw_coeffs_vec(N_total, dev)
-    shares = torch.empty((n, vb), dtype=torch.uint8, device=dev)
+    # The steps rotate over `nbuf` separately allocated share buffers (step i
+    # writes buffer i mod nbuf and reconstructs from it): the split's rate is
+    # a property of its share buffer's physical pages, so
+    # the timed average is over several placements, not one allocation's.
+    nbuf = max(1, args.placements)
+    share_bufs = [torch.empty((n, vb), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
     rec = torch.empty(N, dtype=torch.int64, device=dev)
     w = _native.lagrange(xs, t)
-    share_rows = [shares[x - 1] for x in xs]
+    row_sets = [[sb[x - 1] for x in xs] for sb in share_bufs]
+    for sb in share_bufs:  # first touch of every buffer, before the warm-up
+        _native.split_u64(sec, coeffs, sb, N, t, n)
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
 
-    def step(ev=None):
+    def step(i, ev=None):
+        b = i % nbuf
         if ev:
             ev[0].record(stream)
-        _native.split_u64(sec, coeffs, shares, N, t, n)
+        _native.split_u64(sec, coeffs, share_bufs[b], N, t, n)
         if ev:
             ev[1].record(stream)
-        _native.reconstruct(share_rows, w, out_u64=rec, n=N)
+        _native.reconstruct(row_sets[b], w, out_u64=rec, n=N)
         if ev:
             ev[2].record(stream)
 
     def timed_steps(fn, steps):
-        for _ in range(args.warmup):
-            fn()
+        for i in range(args.warmup):
+            fn(i)
         barrier()
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
         barrier()
         t0 = time.perf_counter()
         for i in range(steps):
-            fn(evs[i])
+            fn(i, evs[i])
         barrier()
         el = time.perf_counter() - t0
         if world > 1:
@@ -887,10 +957,15 @@ def main():
         return el, evs
 
     elapsed, evs = timed_steps(step, args.steps)
-    split_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    split_each = [e[0].elapsed_time(e[1]) for e in evs]
+    split_ms = float(np.mean(split_each))
     recon_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    split_by_buf = [float(np.mean(split_each[b::nbuf])) for b in range(min(nbuf, args.steps))]
 
     # ---- parity of what was timed (cheap, size-independent + sampled) -----
+    last = (args.steps - 1) % nbuf if args.steps else 0
+    shares = share_bufs[last]
+    share_rows = row_sets[last]
     roundtrip = bool(torch.equal(rec, sec))
     sample = min(2048, N)
     from oracle import c_oracle
@@ -900,15 +975,30 @@ def main():
     want = c_oracle.split(sec_h[:sample], co_h, t, n)
     got = np.stack([field.vec_to_limbs(shares[x, : field.vec_bytes(sample)].cpu().numpy(), sample) for x in range(n)])
     oracle_ok = bool(np.array_equal(got, want))
-    all_ok = roundtrip and oracle_ok
+    bufs_equal = all(bool(torch.equal(sb, shares)) for sb in share_bufs)
+    all_ok = roundtrip and oracle_ok and bufs_equal
     if world > 1:  # every rank's parity, not only rank 0's
         fl = torch.tensor([int(all_ok)], dtype=torch.int32, device=cdev)
         torch.distributed.all_reduce(fl, op=torch.distributed.ReduceOp.MIN)
         all_ok = bool(fl.item())
 
-    # ---- same-buffer ceiling: the split's bytes through the same pages -----
-    ceiling = measure_ceiling(dev, sec, coeffs, shares, N, t, n) if N >= (1 << 20) else None
-    recon_ceiling = measure_recon_ceiling(share_rows, rec, N) if N >= (1 << 20) else None
+    # ---- same-buffer ceilings: the split's bytes through the same pages ----
+    split_bytes = N * (8 + (t - 1) * FE_BYTES + n * FE_BYTES)
+    placement = None
+    ceiling = recon_ceiling = None
+    if N >= (1 << 20):
+        fr = [split_bytes / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS for ms in split_by_buf]
+        ceils = [measure_ceiling(dev, sec, coeffs, share_bufs[b], N, t, n) for b in range(len(split_by_buf))]
+        placement = {"buffers": len(split_by_buf), "steps_per_buffer": args.steps // max(1, nbuf),
+                     "split_ms": split_by_buf, "frac": fr, "frac_min": min(fr), "frac_median": float(np.median(fr)),
+                     "frac_max": max(fr), "n_frac_ge_0_70": sum(f >= 0.70 for f in fr),
+                     "ceiling_ms": [c["ms"] for c in ceils],
+                     "split_frac_of_ceiling": [c["ms"] / ms for c, ms in zip(ceils, split_by_buf)]}
+        # over the same buffers the timed average covers: mean of their ceilings
+        ceiling = {"ms": float(np.mean([c["ms"] for c in ceils])), "grid": [c["grid"] for c in ceils],
+                   "kernel": ceils[0]["kernel"], "buffers": len(ceils)}
+        recon_ceiling = measure_recon_ceiling(share_rows, rec, N)
+    del share_bufs, row_sets
 
     # ---- N > 1: the weak-scaling figure (2^log2n elements per GPU) --------
     weak = None
@@ -923,7 +1013,7 @@ def main():
         wrec = torch.empty(N_total, dtype=torch.int64, device=dev)
         wrows = [wsh[x - 1] for x in xs]
 
-        def wstep(ev=None):
+        def wstep(i, ev=None):
             _native.split_u64(wsec, wco, wsh, N_total, t, n)
             _native.reconstruct(wrows, w, out_u64=wrec, n=N_total)
 
@@ -977,12 +1067,16 @@ def main():
                    "parallelism": f"element-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS,
-                     # PMC bytes of the headline launch (2^24, 3-of-5); null for other sizes
+                     # PMC bytes of the headline launch (2^24, 3-of-5) from the committed counter
+                     # passes (not collected by this run); null for other sizes
                      "traffic": ((traffic or {}).get("split_bytes_per_launch")
                                  if abs((traffic or {}).get("split_bytes_per_launch", 0) - split_bytes)
                                  < 0.01 * split_bytes else None),
+                     "traffic_source": (traffic or {}).get("source", os.path.relpath(args.traffic, ROOT)),
                      "kernel": "dn::split_kernel<3, false, false, false, 2>",
                      "algorithmic_bytes_per_launch": split_bytes, "avg_launch_ms": split_ms,
+                     "avg_over": f"{args.steps} timed launches rotating over {nbuf} share buffers",
+                     "placement": placement,
                      "ceiling_measured": ceiling and {
                          **ceiling, "GBps": split_bytes / (ceiling["ms"] * 1e-3) / 1e9,
                          "split_frac_of_ceiling": ceiling["ms"] / split_ms}},

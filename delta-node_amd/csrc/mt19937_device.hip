@@ -33,6 +33,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -640,20 +641,14 @@ void build_levels(uint64_t S, int ki, Level lv[3]) {
 }
 
 // Per-thread host side of a draw: the job tables of the last substream count
-// and length (they depend on S and ki only) and a pinned staging buffer for
-// the small copies (from pageable memory HIP stages every copy through a
-// buffer of its own and the host waits for it).  The buffer is reused only
-// after the previous call's stream synchronize; it is never freed (one per
-// calling thread; at process exit the runtime may be gone before
-// thread-local destructors run).
+// and length (they depend on S and ki only; plain host memory, freed with the
+// thread).
 struct MtHost {
   uint64_t S = ~0ull;
   int ki = -1;
   Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
-  uint32_t* pin = nullptr;
-  size_t pin_words = 0;
 };
 thread_local MtHost tls_mt;
 
@@ -683,16 +678,53 @@ MtHost& mt_levels(uint64_t S, int ki) {
   return H;
 }
 
-uint32_t* mt_pinned(MtHost& h, size_t words) {
-  if (h.pin_words < words) {
-    void* p = nullptr;
-    if (hipHostMalloc(&p, words * 4, hipHostMallocDefault) != hipSuccess) return nullptr;
-    if (h.pin) (void)hipHostFree(h.pin);
-    h.pin = static_cast<uint32_t*>(p);
-    h.pin_words = words;
-  }
-  return h.pin;
+// Pinned staging buffers for a draw's small copies (from pageable memory HIP
+// stages every copy through a buffer of its own and the host waits for it).
+// A process-wide pool: a call leases one for its duration — every call
+// synchronises its stream before it returns, so the buffer is idle again —
+// and gives it back, so the pool holds as many buffers as calls ever ran at
+// once, whatever number of threads made them.  The pool is never destroyed
+// (the HIP runtime may be torn down before static destructors run).
+struct PinPool {
+  std::mutex m;
+  std::vector<std::pair<uint32_t*, size_t>> idle;
+};
+PinPool& pin_pool() {
+  static PinPool* pool = new PinPool;
+  return *pool;
 }
+
+struct PinLease {
+  uint32_t* p = nullptr;
+  size_t words = 0;
+  explicit PinLease(size_t need) {
+    PinPool& pool = pin_pool();
+    {
+      std::lock_guard<std::mutex> g(pool.m);
+      if (!pool.idle.empty()) {
+        auto it = std::max_element(pool.idle.begin(), pool.idle.end(),
+                                   [](const auto& a, const auto& b) { return a.second < b.second; });
+        p = it->first;
+        words = it->second;
+        pool.idle.erase(it);
+      }
+    }
+    if (words < need) {
+      if (p) (void)hipHostFree(p);
+      void* q = nullptr;
+      p = hipHostMalloc(&q, need * 4, hipHostMallocDefault) == hipSuccess ? static_cast<uint32_t*>(q) : nullptr;
+      words = p ? need : 0;
+    }
+  }
+  ~PinLease() {
+    if (!p) return;
+    PinPool& pool = pin_pool();
+    std::lock_guard<std::mutex> g(pool.m);
+    pool.idle.push_back({p, words});
+  }
+  PinLease(const PinLease&) = delete;
+  PinLease& operator=(const PinLease&) = delete;
+};
 
 constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
 
@@ -757,7 +789,8 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   const Level* lv = H.lv;
   const uint64_t njobs = lv[0].jobs.size() + lv[1].jobs.size() + lv[2].jobs.size();
   const size_t w1 = kHead / 4 + kMtN, w2 = kMtN, w3 = H.jobs.size(), wh = 256 / 4 + kMtN;
-  uint32_t* pin = mt_pinned(H, w1 + w2 + w3 + wh);
+  PinLease lease(w1 + w2 + w3 + wh);  // idle again once this call has synchronised its stream
+  uint32_t* pin = lease.p;
   if (!pin) return set_error(DN_ERR_HIP, "%s: pinned staging buffer", name);
   uint32_t *st1 = pin, *st2 = pin + w1, *st3 = st2 + w2, *head = st3 + w3;
   std::memset(st1, 0, kHead);
@@ -843,6 +876,14 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
                          ga.coeffs = static_cast<uint8_t*>(coeffs);
                          launch_gen<0>(ga, s);
                        });
+}
+
+extern "C" int dn_mt19937_split_supported(uint64_t n_elem, int threshold, int n_shares) {
+  if (!(threshold == 2 || threshold == 3 || threshold == 5) || threshold > n_shares || n_shares > DN_MAX_SHARES ||
+      fd_needs_fold(threshold, n_shares))
+    return 0;
+  const uint64_t ncoef = n_elem * static_cast<uint64_t>(threshold - 1);
+  return !ncoef || mt_subs(ncoef) <= mt_jump_max_subs() - 1;
 }
 
 extern "C" int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, const int64_t* secrets, void* shares,

@@ -45,7 +45,7 @@ EXPORTS = (
     "dn_m521_reconstruct", "dn_mt19937_draw_coeffs", "dn_last_error", "dn_version",
     "dn_m521_split_prng", "dn_m521_prng_coeffs",
     "dn_mt19937_device_scratch_bytes", "dn_mt19937_draw_coeffs_device", "dn_mt19937_skip",
-    "dn_mt19937_split_device", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
+    "dn_mt19937_split_device", "dn_mt19937_split_supported", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
 )
 
 
@@ -142,6 +142,8 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_mt19937_split_device.restype = i32
     L.dn_mt19937_split_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), vp, vp, u64,
                                           i32, i32, vp, u64, vp]
+    L.dn_mt19937_split_supported.restype = i32
+    L.dn_mt19937_split_supported.argtypes = [u64, i32, i32]
     L.dn_shamir_make_shares_host.restype = i32
     L.dn_shamir_make_shares_host.argtypes = [ctypes.c_char_p, u64, ctypes.c_char_p, ctypes.c_uint32, i32,
                                              ctypes.c_char_p, ctypes.c_uint32, u64, vp, u64, vp]
@@ -338,6 +340,11 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
     if n == 0:
         return True
     L = lib()
+    if not L.dn_mt19937_split_supported(n, t, n_shares):
+        return False  # before any allocation: the draw, then the split
+    for name, x in (("secrets", secrets), ("shares", shares)):
+        if not x.is_cuda or x.device != shares.device or not x.is_contiguous():
+            raise ValueError(f"mt_split_device: {name} must be a contiguous tensor on the shares' HIP device")
     sb = int(L.dn_mt19937_device_scratch_bytes(n, t - 1))
     scratch = torch.empty(sb, dtype=torch.uint8, device=shares.device)
     version, gauss, state, index = _mt_state(rng)

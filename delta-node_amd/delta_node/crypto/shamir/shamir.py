@@ -264,8 +264,9 @@ class SecretShare(object):
         vb = field.vec_bytes(n)
         if out is None:
             out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
-        elif out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous():
-            raise ValueError(f"make_shares_vec: out must be contiguous uint8 [{shares}, {vb}]")
+        elif (out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous()
+              or out.device != dev):
+            raise ValueError(f"make_shares_vec: out must be contiguous uint8 [{shares}, {vb}] on {dev}")
         if coeffs is None and t > 1 and n > 0 and shares > 0 and _native.mt_split_device(self.random, vals, out, n, t,
                                                                                           shares):
             # fused: the reference's MT19937 draws feed the split in registers (no coefficient block)
@@ -312,8 +313,9 @@ class SecretShare(object):
         vb = field.vec_bytes(n)
         if out is None:
             out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
-        elif out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous():
-            raise ValueError(f"make_shares_vec_prng: out must be contiguous uint8 [{shares}, {vb}]")
+        elif (out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous()
+              or out.device != dev):
+            raise ValueError(f"make_shares_vec_prng: out must be contiguous uint8 [{shares}, {vb}] on {dev}")
         if shares > 0:
             if self.threshold <= 1:
                 _native.split_u64(vals, None, out, n, 1, shares)

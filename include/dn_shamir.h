@@ -209,6 +209,15 @@ int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, const int64_t
                             void* stream);
 
 /*
+ * 1 when dn_mt19937_split_device takes (n_elem, threshold, n_shares) — t in
+ * {2, 3, 5}, t <= n_shares, forward differences without folding, the stream
+ * within the jump table — else 0 (draw, then split).  No allocation, no
+ * device call: lets a caller skip the fused form's scratch allocation when
+ * the call would return DN_ERR_UNSUPPORTED.
+ */
+int dn_mt19937_split_supported(uint64_t n_elem, int threshold, int n_shares);
+
+/*
  * Host.  The byte API for one secret per call (csrc/host_shamir.cpp), the way
  * the reference's callers use it (runner/horizontal/agg.py:142-153,
  * coord/horizontal/agg.py:296,330,362), in any prime field (shamir.py:49-51).

@@ -1,6 +1,6 @@
 """One rank of the multi-rank GPU test (tests/test_gpu_dist.py), run as a fresh
 child process: BASELINE config 4's product path with the gloo backend, every
-rank on cuda:0 —
+rank on cuda:0 (or, with DN_DIST_BACKEND=nccl, RCCL at world size 1) —
 
   dist.draw_coeffs_sharded (device MT19937 jump-ahead to the rank's shard of
   the reference's one coefficient stream) -> the HIP split (split_u64) of the
@@ -34,11 +34,15 @@ def main():
     from delta_node.crypto.shamir import dist as sdist
     from golden.fixtures import chunk_digests, combine_digests, secrets_int64
 
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    res = {"rank": rank, "world": world}
+    backend = os.environ.get("DN_DIST_BACKEND", "gloo")
+    if backend == "nccl":  # RCCL: device tensors move GPU to GPU, no host staging
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    res = {"rank": rank, "world": world, "backend": dist.get_backend()}
     try:
         lo, hi = sdist.shard_range(N, rank, world)
         nl = hi - lo
@@ -56,7 +60,9 @@ def main():
             shares = torch.empty((n, vb), dtype=torch.uint8, device=dev)
             _native.split_u64(sec, coeffs, shares, nl, t, n)
             block[:, :vb].copy_(shares)
+        res["via_host"] = sdist._via_host(block, None)
         full = sdist.allgather_share_blocks(block, N)  # [n, world * B] on every rank
+        res["gathered_on_device"] = bool(full.is_cuda)
         torch.cuda.synchronize()
         fv = full[:, : field.vec_bytes(N)]
         # every rank's random.Random as after ONE sequential draw of the whole stream

@@ -1,0 +1,32 @@
+"""`python3 bench.py --gpus 2` on the GPU box: the parent starts two ranks
+through torch.distributed.run (gloo, both on cuda:0 — the box has one GPU;
+the product backend is RCCL) and prints rank 0's one JSON line, which covers
+ONE 2^20-element vector split + reconstructed over the two ranks (the
+per-element work of shamir.py:55-90, sharded as dist.shard_range)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["DN_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--log2n", "20",
+                        "--rows", "0", "--config4", "0", "--config5", "0", "--cpu-budget", "0",
+                        "--steps", "4", "--warmup", "1", "--placements", "2"],
+                       capture_output=True, text=True, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2
+    assert line["config"]["elements_total"] == 1 << 20
+    assert line["config"]["elements_per_gpu"] == 1 << 19
+    assert line["parity"]["all_ranks_ok"] is True
+    assert line["weak_scaling"]["roundtrip_all_ranks"] is True

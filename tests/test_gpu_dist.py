@@ -36,13 +36,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(world, N, t, n, mt_seed, sec_seed, tmp_path):
+def run_ranks(world, N, t, n, mt_seed, sec_seed, tmp_path, backend="gloo"):
     port = _free_port()
     out = str(tmp_path / "res.json")
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), DN_DIST_BACKEND=backend)
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "gpu_dist_worker.py"), out,
                                        str(N), str(t), str(n), str(mt_seed), str(sec_seed)], env=env))
     try:
@@ -67,6 +67,20 @@ def test_config4_two_ranks_equal_reference_digest(tmp_path):
     assert res[0]["block_equal_single"]
     for r in res:
         assert r["device_draw"] and r["state_equal"] and r["roundtrip"], r
+
+
+def test_config4_rccl_branch_world1_equal_reference_digest(tmp_path):
+    """dist.py's RCCL branch on hardware: a fresh rank with
+    init_process_group("nccl") on cuda:0 (world size 1 — the box has one GPU)
+    runs draw_coeffs_sharded (its rejection flag all-reduced on the device),
+    the HIP split and allgather_share_blocks with device tensors (no host
+    staging); the gathered 5-of-9 block's digest is the reference's."""
+    d = [d for d in manifest()["digests"] if d["name"] == "split_t5n9_2e16"][0]
+    res = run_ranks(1, d["N"], d["t"], d["n"], d["mt_seed"], d["secret_seed"], tmp_path, backend="nccl")[0]
+    assert res["backend"] == "nccl"
+    assert res["via_host"] is False and res["gathered_on_device"] is True
+    assert res["digest"] == d["digest"]
+    assert res["block_equal_single"] and res["device_draw"] and res["state_equal"] and res["roundtrip"], res
 
 
 @pytest.mark.parametrize("world,N,t,n", [(2, 65536 + 300, 5, 9), (3, 100001, 3, 5)])

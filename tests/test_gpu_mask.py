@@ -46,12 +46,15 @@ def test_make_mask_ragged_vs_numpy(n):
     assert np.array_equal(utils.make_mask(seed, (n,)), pm.make_mask_numpy(seed, (n,)))
 
 
-def test_masked_sum_matches_reference_composition():
-    """runner mask_result (agg.py:284-318): fix_precision(val) + seed_mask + sum(+-mask)."""
+@pytest.mark.parametrize("k", [12, 16, 19])
+def test_masked_sum_matches_reference_composition(k):
+    """runner mask_result (agg.py:284-318): fix_precision(val) + seed_mask + sum(+-mask).
+    k = 16 fills one launch's generator slots (the full 64-KB dynamic LDS);
+    k = 19 takes two launches."""
     rng = np.random.default_rng(3)
     val = rng.standard_normal((37, 129)) * 100
-    seeds = [os.urandom(32) for _ in range(12)]  # > 8: two generator groups
-    signs = [1] + [(-1) ** i for i in range(11)]
+    seeds = [os.urandom(32) for _ in range(k)]
+    signs = [1] + [(-1) ** i for i in range(k - 1)]
     terms = list(zip(seeds, signs))
     got = utils.masked_sum(torch.from_numpy(val), terms, precision=8).cpu().numpy()
     want = pm.fix_precision(val, 8)
@@ -96,6 +99,14 @@ def test_exact_replay_on_rejections():
     r1 = np.random.default_rng(list(seed)).integers(low, high, size=20000, dtype=np.int64)
     r2 = np.random.default_rng(list(s2)).integers(low, high, size=20000, dtype=np.int64)
     assert np.array_equal(got, np.arange(20000, dtype=np.int64) + r1 - r2)
+    # the subtracted generator listed first: the kernel sorts generators by
+    # sign, so its reject flags must map back to the caller's order
+    got = bounded_sum([(s2, -1), (seed, 1)], 20000, low, high, base_i64=base).cpu().numpy()
+    assert np.array_equal(got, np.arange(20000, dtype=np.int64) + r1 - r2)
+    s3 = os.urandom(32)
+    r3 = np.random.default_rng(list(s3)).integers(low, high, size=20000, dtype=np.int64)
+    got = bounded_sum([(s2, -1), (s3, -1), (seed, 1)], 20000, low, high).cpu().numpy()
+    assert np.array_equal(got, r1 - r2 - r3)
 
 
 def test_fix_unfix_precision_match_numpy_semantics():

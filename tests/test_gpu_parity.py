@@ -511,3 +511,27 @@ def test_fused_draw_split_from_concurrent_threads():
     for i in range(len(sizes)):
         assert par_st[i] == seq_st[i]
         assert all(torch.equal(a, b) for a, b in zip(par[i], seq[i]))
+
+
+def test_vector_split_rejects_out_off_the_device():
+    """A caller-supplied `out` must live on the current HIP device: a host
+    tensor would hand host pointers to the kernels."""
+    ss = shamir.SecretShare(3)
+    ss.random.seed(5)
+    vals = torch.arange(1000, dtype=torch.int64)
+    out = torch.empty((5, field.vec_bytes(1000)), dtype=torch.uint8)  # host memory
+    state = ss.random.getstate()
+    with pytest.raises(ValueError):
+        ss.make_shares_vec(vals, 5, out=out)
+    with pytest.raises(ValueError):
+        ss.make_shares_vec_prng(vals, 5, out=out)
+    assert ss.random.getstate() == state  # nothing drawn
+    # unsupported fused shapes (t = 4) take the draw + split without the fused scratch
+    ss4 = shamir.SecretShare(4)
+    ss4.random.seed(5)
+    ref = shamir.SecretShare(4)
+    ref.random.seed(5)
+    got = ss4.make_shares_vec(vals, 6)
+    want = torch.empty_like(got)
+    _native.split_u64(vals.to(got.device), ref.draw_coeffs_vec(1000, got.device), want, 1000, 4, 6)
+    assert torch.equal(got, want) and ss4.random.getstate() == ref.random.getstate()

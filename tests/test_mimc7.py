@@ -82,6 +82,25 @@ def test_constant_matches_reference_values():
     assert constant.data_block_size() == 128
 
 
+def test_constant_literals_equal_library_params():
+    """utils/constant.py holds plain literals (importable without the native
+    library, as the reference's); the kernels' copy must be the same."""
+    import ctypes
+
+    from delta_node.crypto.shamir import _native
+    from delta_node.utils import constant
+
+    L = _native.lib()
+    qb = (ctypes.c_uint32 * 8)()
+    cb = (ctypes.c_uint32 * (13 * 8))()
+    L.dn_mimc7_params.restype = ctypes.c_int
+    L.dn_mimc7_params.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    assert L.dn_mimc7_params(ctypes.addressof(qb), ctypes.addressof(cb)) == 0
+    assert int.from_bytes(bytes(qb), "little") == constant.q()
+    raw = bytes(cb)
+    assert [int.from_bytes(raw[32 * i:32 * (i + 1)], "little") for i in range(13)] == constant.cts()
+
+
 def test_calc_commitment_and_npz_helpers(tmp_path):
     import hashlib
     import io
