@@ -518,8 +518,8 @@ def test_vector_split_rejects_out_off_the_device():
     tensor would hand host pointers to the kernels."""
     ss = shamir.SecretShare(3)
     ss.random.seed(5)
-    vals = torch.arange(1000, dtype=torch.int64)
-    out = torch.empty((5, field.vec_bytes(1000)), dtype=torch.uint8)  # host memory
+    vals = torch.arange(1024, dtype=torch.int64)
+    out = torch.empty((5, field.vec_bytes(1024)), dtype=torch.uint8)  # host memory
     state = ss.random.getstate()
     with pytest.raises(ValueError):
         ss.make_shares_vec(vals, 5, out=out)
@@ -533,5 +533,5 @@ def test_vector_split_rejects_out_off_the_device():
     ref.random.seed(5)
     got = ss4.make_shares_vec(vals, 6)
     want = torch.empty_like(got)
-    _native.split_u64(vals.to(got.device), ref.draw_coeffs_vec(1000, got.device), want, 1000, 4, 6)
+    _native.split_u64(vals.to(got.device), ref.draw_coeffs_vec(1024, got.device), want, 1024, 4, 6)
     assert torch.equal(got, want) and ss4.random.getstate() == ref.random.getstate()
