@@ -194,7 +194,7 @@ def measure_recon_ceiling(share_rows, rec, N: int, reps: int = 5) -> dict:
     return best
 
 
-def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int = 5) -> dict:
+def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int = 5, dist_on: bool = False) -> dict:
     """BASELINE config 4: 5-of-9 split of a 2^26-element vector sharded by
     element across the ranks (rank r: `dist.shard_range`), then one RCCL
     all-gather of the per-rank share blocks (world > 1), timed separately.
@@ -220,7 +220,7 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
 
     ss = _shamir.SecretShare(t)
     ss.random.seed(4321)
-    if world > 1:
+    if dist_on:
         cb = sdist.draw_coeffs_sharded(ss, N_total, dev)
         coeffs = cb[:, :vb].contiguous() if cb.shape[1] != vb else cb
     else:
@@ -251,7 +251,7 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
            "roofline": roof("hbm", nl * per_elem / (split_ms * 1e-3) / 1e9,
                             f"8 B secret + {t - 1} x 66 B coefficients + {n} x 66 B shares per element"),
            "roundtrip_equal": ok}
-    if world > 1:
+    if dist_on:
         import torch.distributed as tdist
 
         cdev = dev if tdist.get_backend() == "nccl" else torch.device("cpu")
@@ -868,7 +868,10 @@ def main():
             sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under a launcher the ranks form a process group even at WORLD_SIZE=1, so
+    # the collective code paths (RCCL under nccl) run at every N
+    dist_on = "WORLD_SIZE" in os.environ
+    if dist_on:
         import torch.distributed as dist
 
         # DN_DIST_BACKEND=gloo rehearses the multi-rank control flow on a
@@ -882,7 +885,7 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", torch.cuda.current_device())
     # small control-plane tensors (timings, parity flags): device under nccl, host under gloo
-    cdev = dev if world == 1 or torch.distributed.get_backend() == "nccl" else torch.device("cpu")
+    cdev = dev if not dist_on or torch.distributed.get_backend() == "nccl" else torch.device("cpu")
 
     from delta_node.crypto import shamir
     from delta_node.crypto.shamir import _native, field
@@ -897,7 +900,7 @@ def main():
     N = hi - lo
 
     def barrier():
-        if world > 1:
+        if dist_on:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
@@ -910,7 +913,7 @@ def main():
     sec_h = secrets_int64(1, N_total)[lo:hi].copy()
     sec = torch.from_numpy(sec_h).to(dev)
     vb = field.vec_bytes(N)
-    if world > 1:
+    if dist_on:
         coeffs = sdist.draw_coeffs_sharded(ss, N_total, dev)[:, :vb].contiguous()
     else:
         coeffs = ss.draw_coeffs_vec(N_total, dev)
@@ -950,7 +953,7 @@ def main():
             fn(i, evs[i])
         barrier()
         el = time.perf_counter() - t0
-        if world > 1:
+        if dist_on:
             tt = torch.tensor([el], dtype=torch.float64, device=cdev)
             torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
             el = float(tt.item())
@@ -977,7 +980,7 @@ def main():
     oracle_ok = bool(np.array_equal(got, want))
     bufs_equal = all(bool(torch.equal(sb, shares)) for sb in share_bufs)
     all_ok = roundtrip and oracle_ok and bufs_equal
-    if world > 1:  # every rank's parity, not only rank 0's
+    if dist_on:  # every rank's parity, not only rank 0's
         fl = torch.tensor([int(all_ok)], dtype=torch.int32, device=cdev)
         torch.distributed.all_reduce(fl, op=torch.distributed.ReduceOp.MIN)
         all_ok = bool(fl.item())
@@ -1097,7 +1100,7 @@ def main():
         if world == 1:
             del shares, coeffs, share_rows
         torch.cuda.empty_cache()
-        line["config4"] = config4_bench(dev, world, rank, args.config4_log2n)
+        line["config4"] = config4_bench(dev, world, rank, args.config4_log2n, dist_on=dist_on)
     if args.rows and world == 1:
         line["rows"] = rows_bench(dev, args.log2n)
         line["rows"]["draw_split"] = draw_split_row(dev, args.log2n)
@@ -1108,7 +1111,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(t, n, xs, args.cpu_budget)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         torch.distributed.destroy_process_group()
     if not all_ok:
         sys.exit(3)

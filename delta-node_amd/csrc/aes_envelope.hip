@@ -40,6 +40,12 @@
 #include "dn_aes.h"
 #include "dn_internal.hpp"
 
+// DN_AES_SDWA (default 1): round lookups address LDS through SDWA byte moves
+// (aes_block); 0 builds the v_perm form (the A/B baseline, `make variant`).
+#ifndef DN_AES_SDWA
+#define DN_AES_SDWA 1
+#endif
+
 namespace dn {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -143,10 +149,62 @@ __device__ __forceinline__ uint32_t sub_col(const AesLds<NTAB>& L, const uint32_
   return hi ^ lo ^ k;
 }
 
+// Te_T[byte K of s] with the LDS address built by one SDWA v_mov (VOP1, a
+// full-rate slot) instead of a v_perm (VOP3): byte 1 of this lookup's own
+// address register ar — its lane and table-pair bits set once — is
+// overwritten with byte K of s (dst_unused:UNUSED_PRESERVE keeps the rest).
+// Each of a round's 16 lookups has its own register, so a register is
+// rewritten a whole round after the read that used it.
+template <int K>
+__device__ __forceinline__ void addr_byte(uint32_t& ar, uint32_t s) {
+  if constexpr (K == 0) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(ar) : "v"(s));
+  else if constexpr (K == 1) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(ar) : "v"(s));
+  else if constexpr (K == 2) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(ar) : "v"(s));
+  else asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(ar) : "v"(s));
+}
+
+template <int K, int T>
+__device__ __forceinline__ uint32_t te_sdwa(const AesLds<4>& L, uint32_t s, uint32_t& ar) {
+  addr_byte<K>(ar, s);
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&L.tab[0][0][0]) + ar + 128 * (T & 1));
+}
+
 template <int NR, int NTAB>
 __device__ __forceinline__ void aes_block(const AesLds<NTAB>& L, const uint32_t lw[2], const AesArgs& a,
                                           uint32_t s[4]) {
   uint32_t s0 = s[0] ^ a.rk[0], s1 = s[1] ^ a.rk[1], s2 = s[2] ^ a.rk[2], s3 = s[3] ^ a.rk[3];
+#if DN_AES_SDWA
+  if constexpr (NTAB == 4) {
+    uint32_t ar[4][4];  // [column][table]: lane bits | table pair (T / 2) << 16
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ar[c][t] = lw[t >> 1];
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+      // the round's 16 lookups issued back to back, then the XORs
+      uint32_t x[4][4];
+      const uint32_t st[4] = {s0, s1, s2, s3};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        x[c][0] = te_sdwa<3, 0>(L, st[c], ar[c][0]);
+        x[c][1] = te_sdwa<2, 1>(L, st[(c + 1) & 3], ar[c][1]);
+        x[c][2] = te_sdwa<1, 2>(L, st[(c + 2) & 3], ar[c][2]);
+        x[c][3] = te_sdwa<0, 3>(L, st[(c + 3) & 3], ar[c][3]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      s0 = x[0][0] ^ x[0][1] ^ x[0][2] ^ x[0][3] ^ a.rk[4 * r];
+      s1 = x[1][0] ^ x[1][1] ^ x[1][2] ^ x[1][3] ^ a.rk[4 * r + 1];
+      s2 = x[2][0] ^ x[2][1] ^ x[2][2] ^ x[2][3] ^ a.rk[4 * r + 2];
+      s3 = x[3][0] ^ x[3][1] ^ x[3][2] ^ x[3][3] ^ a.rk[4 * r + 3];
+    }
+    s[0] = sub_col(L, lw, s0, s1, s2, s3, a.rk[4 * NR]);
+    s[1] = sub_col(L, lw, s1, s2, s3, s0, a.rk[4 * NR + 1]);
+    s[2] = sub_col(L, lw, s2, s3, s0, s1, a.rk[4 * NR + 2]);
+    s[3] = sub_col(L, lw, s3, s0, s1, s2, a.rk[4 * NR + 3]);
+    return;
+  }
+#endif
 #pragma unroll
   for (int r = 1; r < NR; ++r) {
     const uint32_t t0 = mix_col(L, lw, s0, s1, s2, s3, a.rk[4 * r]);
@@ -183,30 +241,37 @@ __device__ __forceinline__ void shift_words(const uint32_t* r, uint32_t sb, uint
 }
 
 // 16 NV bytes of the stream at byte `off` (a multiple of 16) of data = base + skew,
-// as little-endian words.  With skew != 0 the NV + 1 aligned vectors read all
-// hold wanted bytes (no read past the 16-byte chunk of the last one).
+// as little-endian words: load_raw issues the aligned vector loads (NV, or NV + 1
+// with skew != 0 — all hold wanted bytes, none is read past the 16-byte chunk of
+// the last one), shift_raw funnel-shifts them into place.  Split so that a loop
+// can issue the next unit's loads before this unit's stores: loads and stores
+// retire in issue order (one vmcnt), so a load issued after a store waits for it.
 template <int NV>
-__device__ __forceinline__ void load_stream(const uint8_t* base, uint32_t skew, uint64_t off, uint32_t* w) {
+__device__ __forceinline__ void load_raw(const uint8_t* base, uint32_t skew, uint64_t off, uint32_t (&r)[4 * NV + 4]) {
   const u32x4* p = reinterpret_cast<const u32x4*>(base + off);
-  if (skew == 0u) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const u32x4 x = __builtin_nontemporal_load(p + v);
-      w[4 * v] = x.x;
-      w[4 * v + 1] = x.y;
-      w[4 * v + 2] = x.z;
-      w[4 * v + 3] = x.w;
-    }
-    return;
-  }
-  uint32_t r[4 * NV + 4];
-#pragma unroll
-  for (int v = 0; v <= NV; ++v) {
+  for (int v = 0; v < NV; ++v) {
     const u32x4 x = __builtin_nontemporal_load(p + v);
     r[4 * v] = x.x;
     r[4 * v + 1] = x.y;
     r[4 * v + 2] = x.z;
     r[4 * v + 3] = x.w;
+  }
+  if (skew != 0u) {
+    const u32x4 x = __builtin_nontemporal_load(p + NV);
+    r[4 * NV] = x.x;
+    r[4 * NV + 1] = x.y;
+    r[4 * NV + 2] = x.z;
+    r[4 * NV + 3] = x.w;
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void shift_raw(const uint32_t (&r)[4 * NV + 4], uint32_t skew, uint32_t* w) {
+  if (skew == 0u) {
+#pragma unroll
+    for (int i = 0; i < 4 * NV; ++i) w[i] = r[i];
+    return;
   }
   const uint32_t sb = skew & 3u;
   switch (skew >> 2) {
@@ -215,6 +280,13 @@ __device__ __forceinline__ void load_stream(const uint8_t* base, uint32_t skew, 
     case 2: shift_words<2, NV>(r, sb, w); break;
     default: shift_words<3, NV>(r, sb, w); break;
   }
+}
+
+template <int NV>
+__device__ __forceinline__ void load_stream(const uint8_t* base, uint32_t skew, uint64_t off, uint32_t* w) {
+  uint32_t r[4 * NV + 4];
+  load_raw<NV>(base, skew, off, r);
+  shift_raw<NV>(r, skew, w);
 }
 
 __device__ __forceinline__ void store4(uint8_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
@@ -274,6 +346,18 @@ __device__ __forceinline__ void hex_word(uint32_t c, uint32_t& h0, uint32_t& h1)
   h1 = hex_digits(__builtin_amdgcn_perm(hi, lo, 0x03070206u));
 }
 
+// hex_word for base64 characters only (A-Z a-z 0-9 + /, all in 0x2B..0x7A):
+// every high nibble is 2..7, a decimal digit, so only the low nibbles take
+// the letter test
+__device__ __forceinline__ void hex_word_b64(uint32_t c, uint32_t& h0, uint32_t& h1) {
+  uint32_t hi;
+  // (c >> 4) & 0x0F0F0F0F | 0x30303030 in one v_bitop3 ((S0 & S1) | S2: table 0xea; one SGPR operand)
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(hi) : "v"(c >> 4), "s"(0x0F0F0F0Fu), "v"(0x30303030u));
+  const uint32_t lo = hex_digits(c & 0x0F0F0F0Fu);
+  h0 = __builtin_amdgcn_perm(hi, lo, 0x01050004u);
+  h1 = __builtin_amdgcn_perm(hi, lo, 0x03070206u);
+}
+
 // 4 hex digits (one per byte) -> 4 nibble values; bad |= non-hex bytes
 __device__ __forceinline__ uint32_t unhex4(uint32_t c, uint32_t& bad) {
   const uint32_t c7 = c & 0x7F7F7F7Fu, l7 = c7 | 0x20202020u;
@@ -330,13 +414,17 @@ template <int NR, int NTAB>
 __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) ctr_kernel(const AesArgs a) {
   DN_AES_PROLOGUE;
   const uint8_t* in = a.in + a.skew;
+  uint32_t R[8];  // raw loads of the next whole block, issued before this block's store
+  if (first < a.units && 16 * (first + 1) <= a.n) load_raw<1>(a.in, a.skew, 16 * first, R);
   for (uint64_t b = first; b < a.units; b += stride) {
     uint32_t ks[4];
     ctr_block(a.iv, b, ks);
     aes_block<NR>(L, lw, a, ks);
     if (16 * (b + 1) <= a.n) {
       uint32_t p[4];
-      load_stream<1>(a.in, a.skew, 16 * b, p);
+      shift_raw<1>(R, a.skew, p);
+      const uint64_t bn = b + stride;
+      if (bn < a.units && 16 * (bn + 1) <= a.n) load_raw<1>(a.in, a.skew, 16 * bn, R);
       store4(a.out + 16 * b, p[0] ^ __builtin_bswap32(ks[0]), p[1] ^ __builtin_bswap32(ks[1]),
              p[2] ^ __builtin_bswap32(ks[2]), p[3] ^ __builtin_bswap32(ks[3]));
     } else {
@@ -406,13 +494,20 @@ template <int NR, int NTAB, bool HEX>
 __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const AesArgs a) {
   DN_AES_PROLOGUE;
   const uint64_t m = a.n + 16;
+  // plaintext of blocks 3g-1 .. 3g+1 of the next whole unit, loaded before this unit's stores
+  uint32_t R[16];
+  if (first < a.units && first != 0 && 48 * (first + 1) <= m) load_raw<3>(a.in, a.skew, 48 * first - 16, R);
   for (uint64_t g = first; g < a.units; g += stride) {
+    const uint64_t gn = g + stride;
+    const bool next_whole = gn < a.units && 48 * (gn + 1) <= m;
     if (g == 0 || 48 * (g + 1) > m) {
       encrypt_unit_slow<NR, NTAB, HEX>(L, lw, a, g);
+      if (next_whole) load_raw<3>(a.in, a.skew, 48 * gn - 16, R);
       continue;
     }
     uint32_t W[12];
-    load_stream<3>(a.in, a.skew, 48 * g - 16, W);  // plaintext of blocks 3g-1 .. 3g+1
+    shift_raw<3>(R, a.skew, W);
+    if (next_whole) load_raw<3>(a.in, a.skew, 48 * gn - 16, R);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       uint32_t ks[4];
@@ -428,8 +523,8 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
 #pragma unroll
       for (int v = 0; v < 8; ++v) {
         uint32_t h0, h1, h2, h3;
-        hex_word(C[2 * v], h0, h1);
-        hex_word(C[2 * v + 1], h2, h3);
+        hex_word_b64(C[2 * v], h0, h1);
+        hex_word_b64(C[2 * v + 1], h2, h3);
         store4(o + 16 * v, h0, h1, h2, h3, a.plain != 0u);
       }
     } else {

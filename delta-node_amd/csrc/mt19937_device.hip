@@ -347,18 +347,122 @@ struct GenArgs {
   uint8_t* shares;
   uint64_t n_elem;
   int32_t n_shares;
-  uint32_t ring;         // ring words of one wave (2 emission groups)
+  uint32_t ring;         // ring slots of one wave (2 emission groups; GenRing)
 };
 
-// 64 draws of one group (lane = draw c of this substream, words 17 c .. 17 c +
-// 16 of the ring at `rb` words): +1, rejection test, tiled store.
+// Raw (untempered) words of a substream pass through an LDS ring of M words
+// (M = two emission groups): stream word p sits at slot (p + delta) mod M,
+// physical word o + slot, and physical words [o + M, o + M + 64) mirror slots
+// [0, 64).
+//  * An append writes the 64 words p0 .. p0 + 63 (p0 + delta a multiple of
+//    64, so its slots never wrap), word p = mix(word p - 624, word p - 623,
+//    word p - 227): one address plus immediates, except in the first 688
+//    slots of the ring, where the three operands' slots wrap per lane (a
+//    wave-uniform branch, 11 of 68 appends at t = 3).
+//  * An emission group [g G, (g + 1) G) reads physical o + delta + (g % 2) G
+//    onwards, below o + M + 64: the mirror holds the slots past M.
+// delta is 0 except in substream 0, whose stream starts with the caller's
+// 624 - idx words; o = delta & 1 keeps every group's first word 8-byte aligned
+// (the emission's b64 reads).  Tempering happens when a group is emitted.
+// Per 64 words an append is one address add, three ds_read_b32, the mix
+// (5 VALU) and one ds_write — against three ds_bpermute, their operand
+// selects, the mix, the temper and the ring address arithmetic of a
+// register-resident window.
+struct GenRing {
+  uint32_t M, delta, o;
+};
+
+__device__ __forceinline__ uint32_t ring_wrap(uint32_t s, uint32_t M) { return s >= M ? s - M : s; }
+
+// mt_mix in five VALU: y = bfi(UP, a, b); m ^ (y >> 1) ^ (-(b & 1) & A), the
+// last two terms by v_bitop3 ((S0 & S1) ^ S2, table 0x6a; S0 the index MSB).
+__device__ __forceinline__ uint32_t mt_mix5(uint32_t a, uint32_t b, uint32_t m) {
+  uint32_t y, r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(y) : "s"(kMtUp), "v"(a), "v"(b));
+  const uint32_t u = (y >> 1) ^ m;
+  const uint32_t mk = static_cast<uint32_t>(static_cast<int32_t>(b << 31) >> 31);
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(r) : "v"(mk), "s"(kMtA), "v"(u));
+  return r;
+}
+
+// B appends (B <= 3: the appends of a batch read no word another one of the
+// batch writes: word p + 64 i - 227 < p for i < 3), reads first, one wait.
+// WRAP: some operand slots of the batch lie below 0 (the batch starts in the
+// ring's first 688 slots, or the batch itself wraps) and are wrapped per lane.
+// vals: the raw words (the final-state wave keeps them).
+template <int B, bool WRAP>
+__device__ __forceinline__ void ring_appends(uint32_t* Rg, const GenRing& g, uint32_t slot, uint32_t lane,
+                                             uint32_t (&vals)[3]) {
+  uint32_t s[B], xa[B], xb[B], xm[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    if constexpr (WRAP) {
+      s[i] = ring_wrap(slot + 64u * i, g.M);
+      const uint32_t q = s[i] + lane;
+      const uint32_t qa = q < 624u ? q + g.M - 624u : q - 624u;
+      const uint32_t qb = qa + 1u == g.M ? 0u : qa + 1u;
+      const uint32_t qm = q < 227u ? q + g.M - 227u : q - 227u;
+      xa[i] = Rg[g.o + qa];
+      xb[i] = Rg[g.o + qb];
+      xm[i] = Rg[g.o + qm];
+    } else {
+      s[i] = slot + 64u * i;
+      const uint32_t* p = Rg + (g.o + s[i] - 624u) + lane;
+      xa[i] = p[0];
+      xb[i] = p[1];
+      xm[i] = p[kMtM];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every read of the batch issued before the first mix waits
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    const uint32_t v = mt_mix5(xa[i], xb[i], xm[i]);
+    vals[i] = v;
+    Rg[g.o + s[i] + lane] = v;
+    if (WRAP && s[i] == 0u) Rg[g.o + g.M + lane] = v;  // mirror of slots 0 .. 63
+  }
+}
+
+template <int B>
+__device__ __forceinline__ void ring_batch(uint32_t* Rg, const GenRing& g, uint32_t& slot, uint32_t lane,
+                                           uint32_t (&vals)[3]) {
+  const uint32_t s0 = __builtin_amdgcn_readfirstlane(slot);
+  if (s0 >= 688u && s0 + 64u * B <= g.M) ring_appends<B, false>(Rg, g, s0, lane, vals);
+  else ring_appends<B, true>(Rg, g, s0, lane, vals);
+  slot = __builtin_amdgcn_readfirstlane(ring_wrap(s0 + 64u * B, g.M));
+}
+
+// NA appends as batches of three (one of one or two last).
+template <int NA>
+__device__ __forceinline__ void ring_run(uint32_t* Rg, const GenRing& g, uint32_t& slot, uint32_t lane) {
+  uint32_t v[3];
+#pragma unroll
+  for (int k = 0; k + 3 <= NA; k += 3) ring_batch<3>(Rg, g, slot, lane, v);
+  if constexpr (NA % 3) ring_batch<NA % 3>(Rg, g, slot, lane, v);
+}
+
+// The window (624 raw words at stream positions [p_start - 624, p_start))
+// into the ring, with the mirror.
+__device__ __forceinline__ void ring_init(uint32_t* Rg, const GenRing& g, const uint32_t* win, uint32_t p_start,
+                                          uint32_t lane) {
+  for (uint32_t i = lane; i < static_cast<uint32_t>(kMtN); i += 64u) {
+    // slot of position p_start - 624 + i, in [0, M)
+    const uint32_t s = (p_start + g.delta + g.M - static_cast<uint32_t>(kMtN) + i) % g.M;
+    const uint32_t v = win[i];
+    Rg[g.o + s] = v;
+    if (s < 64u) Rg[g.o + g.M + s] = v;
+  }
+}
+
+// 64 draws of one group (lane = draw c of this substream, raw words 17 c ..
+// 17 c + 16 of the group at `rb`): temper, +1, rejection test, tiled store.
 __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb, uint64_t qb, uint32_t rbm,
                                           uint32_t c, uint32_t nloc, uint32_t lane) {
   if (c >= nloc) return;
   uint32_t v[kLimbs];  // (the group's ring slice is 64 draws of 17 words)
   const uint32_t* w = rb + 17u * lane;
 #pragma unroll
-  for (int i = 0; i < kLimbs; ++i) v[i] = w[i];
+  for (int i = 0; i < kLimbs; ++i) v[i] = mt_temper(w[i]);
   v[16] >>= 23;
   uint32_t all = v[1];
 #pragma unroll
@@ -379,27 +483,14 @@ __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb,
   __builtin_nontemporal_store(static_cast<uint16_t>(v[16]), reinterpret_cast<uint16_t*>(tb + kHiOffset) + wl);
 }
 
-template <int... ks>
-__device__ __forceinline__ void gen_run(uint32_t (&Q)[11], const Lanes& L, uint32_t* R, uint32_t ring, uint32_t& wpos,
-                                        std::integer_sequence<int, ks...>) {
-  // each append: temper the 64 new words into the ring at stream word wpos
-  ((void)[&] {
-     const uint32_t t = mt_temper(append64<ks>(Q, L));
-     uint32_t pos = wpos + (threadIdx.x & 63u);
-     pos = pos >= ring ? pos - ring : pos;
-     R[pos] = t;
-     wpos = wpos + 64u >= ring ? wpos + 64u - ring : wpos + 64u;
-   }(),
-   ...);
-}
-
 // Fused split (T = t): the 64 elements of one group (lane = element, 64 (t-1)
 // consecutive draws of this substream, element-major as make_shares draws
-// them: words 17 ((t-1) lane + j - 1) .. + 16 of the group for coefficient j),
-// their int64 secrets, and the split of split_kernel<T, false, false>: the
-// forward-difference table stored share by share.
-template <int T>
-__device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t ebase, uint32_t lane) {
+// them: raw words 17 ((t-1) lane + j - 1) .. + 16 of the group for
+// coefficient j), their int64 secrets, and the split of split_kernel<T,
+// false, false>: the forward-difference table stored share by share.
+template <int T, int SAUX, int NS, bool WHOLE>
+__device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t ebase, uint32_t lane,
+                                           uint64_t s) {
   constexpr int TM1 = T - 1;
   // ebase (the group's first element) is wave-uniform and a multiple of 64, so
   // the group's 64 elements share one tile: its index is a scalar and every
@@ -407,7 +498,7 @@ __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb,
   // descriptor, no waterfall loop around the stores)
   const uint32_t tile = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ebase >> 8));
   const uint64_t e = ebase + lane;
-  if (e >= a.n_elem) return;
+  if (!WHOLE && e >= a.n_elem) return;  // WHOLE: every element of the group is in the vector
   uint32_t c[T][kLimbs];
   const uint32_t* w = rb + 17u * TM1 * lane;
   if constexpr (TM1 % 2 == 0) {
@@ -423,12 +514,12 @@ __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb,
 #pragma unroll
     for (int j = 1; j < T; ++j)
 #pragma unroll
-      for (int i = 0; i < kLimbs; ++i) c[j][i] = ww[17 * (j - 1) + i];
+      for (int i = 0; i < kLimbs; ++i) c[j][i] = mt_temper(ww[17 * (j - 1) + i]);
   } else {
 #pragma unroll
     for (int j = 1; j < T; ++j)
 #pragma unroll
-      for (int i = 0; i < kLimbs; ++i) c[j][i] = w[17 * (j - 1) + i];
+      for (int i = 0; i < kLimbs; ++i) c[j][i] = mt_temper(w[17 * (j - 1) + i]);
   }
 #pragma unroll
   for (int j = 1; j < T; ++j) {
@@ -441,36 +532,32 @@ __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb,
 #pragma unroll
     for (int i = 0; i < kLimbs; ++i) c[j][i] = __builtin_addc(c[j][i], 0u, cy, &cy);
   }
-  const uint64_t s = static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + e));
   c[0][0] = static_cast<uint32_t>(s);
   c[0][1] = static_cast<uint32_t>(s >> 32);
 #pragma unroll
   for (int i = 2; i < kLimbs; ++i) c[0][i] = 0u;
   fd_init<T>(c);
   const uint32_t wl = static_cast<uint32_t>(e & 255u);
+  if constexpr (NS > 0) {
+#pragma unroll
+    for (int xi = 1; xi <= NS; ++xi) {
+      store_reduced<SAUX>(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vb, tile)), wl, c[0]);
+      if (xi < NS) fd_step<T>(c);
+    }
+  } else {
 #pragma unroll 1
-  for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
-    store_reduced(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vb, tile)), wl, c[0]);
-    fd_step<T>(c);
+    for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+      store_reduced<SAUX>(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.vb, tile)), wl, c[0]);
+      fd_step<T>(c);
+    }
   }
-}
-
-template <int... ks>
-__device__ __forceinline__ void final_run(uint32_t (&Q)[11], const Lanes& L, uint64_t& np, uint64_t tf,
-                                          uint32_t* fin, std::integer_sequence<int, ks...>) {
-  ((void)[&] {
-     const uint32_t v = append64<ks>(Q, L);
-     const uint64_t x = np + (threadIdx.x & 63u);
-     if (x >= tf && x < tf + kMtN) fin[x - tf] = v;
-     np += 64u;
-   }(),
-   ...);
 }
 
 // One 64-thread workgroup per substream (one extra for CPython's final state):
 // T == 0 stores the coefficients (groups of 64 draws), T > 0 splits the
 // substream's elements (groups of 64 elements) with them as they are drawn.
-template <int T>
+// Dynamic LDS: 1 + ring + 64 words (GenRing).
+template <int T, int SAUX = kNt, int NS = 0>
 __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
   const uint32_t lane = threadIdx.x & 63u;
@@ -479,28 +566,37 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   const bool fin_wave = sub == a.S;
   const uint32_t wsel = fin_wave ? static_cast<uint32_t>(a.final_sig) : sub;
   const uint32_t* win = a.wins + static_cast<uint64_t>(wsel) * kMtN;
-  Lanes L;
-  L.pa = static_cast<int>(((lane + 16u) & 63u) * 4u);
-  L.pb = static_cast<int>(((lane + 17u) & 63u) * 4u);
-  L.pm = static_cast<int>(((lane + 29u) & 63u) * 4u);
-  L.la = lane < 16u, L.lb = lane < 17u, L.lm = lane < 29u;
-  uint32_t Q[11];
-#pragma unroll
-  for (int r = 0; r < 11; ++r) {
-    const int i = 64 * r + static_cast<int>(lane) - 16;
-    Q[r] = (i >= 0 && i < kMtN) ? win[i] : 0u;
-  }
-  const auto run11 = std::make_integer_sequence<int, 11>{};
+  // positions of this substream: word 0 is its first output; the window holds
+  // [p_start - 624, p_start) (substream 0: the caller's array, whose words
+  // idx .. 623 are outputs 0 .. 623 - idx)
+  const uint32_t p_start = (sub == 0 && !fin_wave) ? kMtN - a.idx : 0u;
+  GenRing g;
+  g.M = a.ring;
+  g.delta = (64u - (p_start & 63u)) & 63u;
+  g.o = g.delta & 1u;
+  uint32_t* R = s_ring;
+  ring_init(R, g, win, p_start, lane);
+  uint32_t slot = __builtin_amdgcn_readfirstlane((p_start + g.delta) % g.M);  // slot of the next append
+  wave_sync();
   if (fin_wave) {
-    // step from the window at final_pos until positions tf .. tf + 623 are produced
+    // CPython's final array: positions tf .. tf + 623 of the whole stream,
+    // from the window at position P (its word 0) onwards
     const uint64_t P = a.final_pos, tf = a.final_tf;
     for (uint32_t i = lane; i < static_cast<uint32_t>(kMtN); i += 64u)
       if (P + i >= tf && P + i < tf + kMtN) a.fin[P + i - tf] = win[i];
-    uint64_t np = P + kMtN;
-    while (np < tf + kMtN) final_run(Q, L, np, tf, a.fin, run11);
+    uint64_t np = P + kMtN;  // position of the next append's word 0
+    while (np < tf + kMtN) {
+      uint32_t v[3];
+      ring_batch<3>(R, g, slot, lane, v);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint64_t x = np + 64u * k + lane;
+        if (x >= tf && x < tf + kMtN) a.fin[x - tf] = v[k];
+      }
+      np += 192u;
+    }
     return;
   }
-  uint32_t* R = s_ring;
   const uint32_t group = a.ring / 2u;                            // words per emission group
   const uint64_t k0 = static_cast<uint64_t>(sub) * a.sub_draws;  // first draw of this substream
   const uint32_t nloc = static_cast<uint32_t>(a.ncoef - k0 < a.sub_draws ? a.ncoef - k0 : a.sub_draws);
@@ -508,27 +604,63 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   const uint32_t ngroups = (nloc + gdraws - 1u) / gdraws;
   const uint64_t qb = k0 / static_cast<uint64_t>(a.tm1);
   const uint32_t rbm = static_cast<uint32_t>(k0 - qb * static_cast<uint64_t>(a.tm1));
-  uint32_t wpos = 0;  // ring position of the next stream word of this substream
-  if (sub == 0) {     // the rest of the caller's array comes first
-    const uint32_t h = kMtN - a.idx;
-    for (uint32_t j = lane; j < h; j += 64u) R[j] = mt_temper(win[a.idx + j]);
-    wpos = h;
-  }
-  uint32_t done = 0, have = wpos;  // groups emitted, stream words produced
-  while (done < ngroups) {
-    gen_run(Q, L, R, a.ring, wpos, run11);
-    have += 11u * 64u;
-    wave_sync();
-    while (done < ngroups && have >= (done + 1u) * group) {
-      const uint32_t* rb = R + (done & 1u) * group;
-      if constexpr (T == 0) {
-        emit_group(a, rb, qb, rbm, 64u * done + lane, nloc, lane);
-      } else {
-        emit_split<T>(a, rb, qb + 64u * done, lane);  // k0 / (t-1) = the substream's first element
-      }
-      ++done;
+  constexpr int kRun = 17 * (T ? T - 1 : 1);  // appends per run = one group's words / 64
+  // Every run appends exactly one group's words (have = p_start + runs * group
+  // with p_start < group), so each run is followed by exactly one emission.
+  if constexpr (T == 0) {
+    for (uint32_t done = 0; done < ngroups; ++done) {
+      ring_run<kRun>(R, g, slot, lane);
+      wave_sync();
+      emit_group(a, R + g.o + g.delta + (done & 1u) * group, qb, rbm, 64u * done + lane, nloc, lane);
+      wave_sync();
     }
-    wave_sync();
+  } else {
+    // The int64 secret of this lane's element in the next group is loaded a
+    // group ahead — before the current group's share stores, since loads and
+    // stores retire in issue order and a load issued after them would wait for
+    // them — into one of two registers by group parity (no copy of a pending
+    // load), from an index clamped to the vector (the last prefetch is unused).
+    // With the share count a template argument (NS) and only whole groups
+    // (all 64 elements in the vector) in the loop, the share stores are
+    // straight-line code on every path and the wait before a prefetched
+    // secret's use leaves them in flight (vmcnt(63)); a runtime share loop or a
+    // lane-masked emission gets vmcnt(<= 1).  A last partial group is emitted
+    // after the loop, with a secret loaded at that point.
+    const uint64_t e0 = qb + lane;  // k0 / (t-1) = the substream's first element
+    const uint64_t elast = a.n_elem - 1u;
+    auto secret_of = [&](uint32_t gi) {
+      const uint64_t e = e0 + 64u * gi;
+      return static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + (e < elast ? e : elast)));
+    };
+    const uint64_t rem = a.n_elem - qb;  // elements from this substream's first one to the vector's end
+    const uint32_t nfull = rem >= 64ull * ngroups ? ngroups : static_cast<uint32_t>(rem / 64u);
+    auto step = [&](uint32_t gi, uint64_t cur, uint64_t& nxt) {
+      ring_run<kRun>(R, g, slot, lane);
+      wave_sync();
+      nxt = secret_of(gi + 1u);
+      emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+      wave_sync();
+    };
+    uint64_t secA = secret_of(0), secB = 0;
+    uint32_t gi = 0;
+    if (nfull > 0u) {
+      step(0u, secA, secB);
+      gi = 1u;
+      for (; gi + 1u < nfull; gi += 2u) {
+        step(gi, secB, secA);
+        step(gi + 1u, secA, secB);
+      }
+      if (gi < nfull) {
+        step(gi, secB, secA);
+        ++gi;
+      }
+    }
+    if (gi < ngroups) {  // the vector's last, partial group
+      ring_run<kRun>(R, g, slot, lane);
+      wave_sync();
+      emit_split<T, SAUX, NS, false>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, secret_of(gi));
+    }
+    asm volatile("" : : "v"(secA ^ secB));  // no load left in flight at the end
   }
 }
 
@@ -862,7 +994,23 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
 template <int T>
 void launch_gen(GenArgs& ga, hipStream_t s) {
   ga.ring = 2u * 17u * 64u * (T ? T - 1 : 1);
-  hipLaunchKernelGGL((mt_gen_kernel<T>), dim3(ga.S + 1), dim3(64), ga.ring * 4u, s, ga);
+  const uint32_t lds_words = 1u + ga.ring + 64u;  // GenRing: alignment word, ring, mirror
+#ifdef DN_TUNING
+  // DN_MT_STORE_AUX (tuning build): cache policy bits of the fused split's share stores (t = 3)
+  const char* sa = T == 3 ? tune_env("DN_MT_STORE_AUX") : nullptr;
+  const int aux = sa ? std::atoi(sa) : kNt;
+  if (T == 3 && aux != kNt) {
+    if (aux == 0) hipLaunchKernelGGL((mt_gen_kernel<T, 0>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+    else if (aux == 1) hipLaunchKernelGGL((mt_gen_kernel<T, 1>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+    else if (aux == 16) hipLaunchKernelGGL((mt_gen_kernel<T, 16>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+    else hipLaunchKernelGGL((mt_gen_kernel<T, 18>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+    return;
+  }
+#endif
+  if (T == 3 && ga.n_shares == 5)  // the headline 3-of-5: straight-line share stores (see mt_gen_kernel)
+    hipLaunchKernelGGL((mt_gen_kernel<T, kNt, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+  else
+    hipLaunchKernelGGL((mt_gen_kernel<T>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
 }
 
 }  // namespace

@@ -5,6 +5,7 @@ ONE 2^20-element vector split + reconstructed over the two ranks (the
 per-element work of shamir.py:55-90, sharded as dist.shard_range)."""
 import json
 import os
+import socket
 import subprocess
 import sys
 
@@ -30,3 +31,25 @@ def test_bench_gpus_2_launches_two_ranks():
     assert line["config"]["elements_per_gpu"] == 1 << 19
     assert line["parity"]["all_ranks_ok"] is True
     assert line["weak_scaling"]["roundtrip_all_ranks"] is True
+
+
+def test_bench_under_launcher_world1_rccl():
+    """torch.distributed.run with one rank: bench.py forms an RCCL process
+    group (nccl) at WORLD_SIZE=1, so the sharded MT draw's device all-reduce,
+    the timing / parity all-reduces and config 4's RCCL all-gather run on the
+    GPU."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["DN_DIST_BACKEND"] = "nccl"
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "1", "--log2n", "20", "--rows", "0", "--config4", "1", "--config4-log2n", "20",
+                        "--config5", "0", "--cpu-budget", "0", "--steps", "2", "--warmup", "1", "--placements", "2"],
+                       capture_output=True, text=True, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["parity"]["all_ranks_ok"] is True
+    assert line["config4"]["allgather"]["blocks_equal"] is True
+    assert line["config4"]["allgather"]["all_ranks_ok"] is True
