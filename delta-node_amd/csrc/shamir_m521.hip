@@ -233,6 +233,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
       }
       continue;
     }
+    if constexpr (PRNG) prng_tile_tops<T>(a, tile, lane, tops);
 #pragma unroll 1
     for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
