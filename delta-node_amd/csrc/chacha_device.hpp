@@ -59,48 +59,6 @@ __device__ __forceinline__ void chacha_block(uint32_t x[16], const ChachaKey& K,
   x[12] += c0; x[13] += c1; x[14] += K.n0; x[15] += K.n1;
 }
 
-// Two blocks (counters cx, cy) through the rounds side by side: eight
-// independent quarter-round chains per half round instead of four, for the
-// VALU's dependent-issue latency.  Same results as two chacha_block calls.
-__device__ __forceinline__ void chacha_block2(uint32_t x[16], uint32_t y[16], const ChachaKey& K, uint64_t cx,
-                                              uint64_t cy) {
-  const uint32_t x0 = static_cast<uint32_t>(cx), x1 = static_cast<uint32_t>(cx >> 32);
-  const uint32_t y0 = static_cast<uint32_t>(cy), y1 = static_cast<uint32_t>(cy >> 32);
-  x[0] = y[0] = 0x61707865u; x[1] = y[1] = 0x3320646eu; x[2] = y[2] = 0x79622d32u; x[3] = y[3] = 0x6b206574u;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) x[4 + i] = y[4 + i] = K.k[i];
-  x[12] = x0; x[13] = x1; x[14] = K.n0; x[15] = K.n1;
-  y[12] = y0; y[13] = y1; y[14] = K.n0; y[15] = K.n1;
-#pragma unroll 1
-  for (int r = 0; r < K.rounds; r += 2) {
-    chacha_qr(x[0], x[4], x[8], x[12]);
-    chacha_qr(y[0], y[4], y[8], y[12]);
-    chacha_qr(x[1], x[5], x[9], x[13]);
-    chacha_qr(y[1], y[5], y[9], y[13]);
-    chacha_qr(x[2], x[6], x[10], x[14]);
-    chacha_qr(y[2], y[6], y[10], y[14]);
-    chacha_qr(x[3], x[7], x[11], x[15]);
-    chacha_qr(y[3], y[7], y[11], y[15]);
-    chacha_qr(x[0], x[5], x[10], x[15]);
-    chacha_qr(y[0], y[5], y[10], y[15]);
-    chacha_qr(x[1], x[6], x[11], x[12]);
-    chacha_qr(y[1], y[6], y[11], y[12]);
-    chacha_qr(x[2], x[7], x[8], x[13]);
-    chacha_qr(y[2], y[7], y[8], y[13]);
-    chacha_qr(x[3], x[4], x[9], x[14]);
-    chacha_qr(y[3], y[4], y[9], y[14]);
-  }
-  x[0] += 0x61707865u; x[1] += 0x3320646eu; x[2] += 0x79622d32u; x[3] += 0x6b206574u;
-  y[0] += 0x61707865u; y[1] += 0x3320646eu; y[2] += 0x79622d32u; y[3] += 0x6b206574u;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    x[4 + i] += K.k[i];
-    y[4 + i] += K.k[i];
-  }
-  x[12] += x0; x[13] += x1; x[14] += K.n0; x[15] += K.n1;
-  y[12] += y0; y[13] += y1; y[14] += K.n0; y[15] += K.n1;
-}
-
 // v >= p - 1 (limb 16 already masked to 9 bits).
 __device__ __forceinline__ bool prng_rejected(const uint32_t v[17]) {
   uint32_t all = v[1];

@@ -996,14 +996,17 @@ void launch_gen(GenArgs& ga, hipStream_t s) {
   ga.ring = 2u * 17u * 64u * (T ? T - 1 : 1);
   const uint32_t lds_words = 1u + ga.ring + 64u;  // GenRing: alignment word, ring, mirror
 #ifdef DN_TUNING
-  // DN_MT_STORE_AUX (tuning build): cache policy bits of the fused split's share stores (t = 3)
+  // DN_MT_STORE_AUX (tuning build): cache policy bits of the fused split's share stores (3-of-5)
   const char* sa = T == 3 ? tune_env("DN_MT_STORE_AUX") : nullptr;
-  const int aux = sa ? std::atoi(sa) : kNt;
-  if (T == 3 && aux != kNt) {
-    if (aux == 0) hipLaunchKernelGGL((mt_gen_kernel<T, 0>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
-    else if (aux == 1) hipLaunchKernelGGL((mt_gen_kernel<T, 1>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
-    else if (aux == 16) hipLaunchKernelGGL((mt_gen_kernel<T, 16>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
-    else hipLaunchKernelGGL((mt_gen_kernel<T, 18>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+  if (sa && T == 3 && ga.n_shares == 5) {
+    const int aux = std::atoi(sa);
+    constexpr int NS = T == 3 ? 5 : 0;
+    const dim3 g(ga.S + 1), b(64);
+    if (aux == 0) hipLaunchKernelGGL((mt_gen_kernel<T, 0, NS>), g, b, lds_words * 4u, s, ga);
+    else if (aux == 1) hipLaunchKernelGGL((mt_gen_kernel<T, 1, NS>), g, b, lds_words * 4u, s, ga);
+    else if (aux == 2) hipLaunchKernelGGL((mt_gen_kernel<T, 2, NS>), g, b, lds_words * 4u, s, ga);
+    else if (aux == 16) hipLaunchKernelGGL((mt_gen_kernel<T, 16, NS>), g, b, lds_words * 4u, s, ga);
+    else hipLaunchKernelGGL((mt_gen_kernel<T, 18, NS>), g, b, lds_words * 4u, s, ga);
     return;
   }
 #endif

@@ -44,12 +44,6 @@ struct SplitArgs {
   ChachaKey key;         // PRNG coefficients: key, nonce, rounds
 };
 
-// DN_PRNG_X2 (default 1): the device-PRNG split draws its coefficient blocks in
-// pairs (chacha_block2); 0 builds one block at a time (the A/B baseline).
-#ifndef DN_PRNG_X2
-#define DN_PRNG_X2 1
-#endif
-
 constexpr int kBlock = 256;  // 4 waves
 constexpr int kWavesPerBlock = kBlock / 64;
 constexpr uint32_t kXcds = 8;
@@ -145,18 +139,10 @@ template <int T>
 __device__ __forceinline__ void prng_coeffs_of(const SplitArgs& a, uint32_t tile, uint32_t w, const uint32_t* tops,
                                                uint32_t c[T][kLimbs]) {
   const uint64_t g = a.elem_offset + static_cast<uint64_t>(tile) * kTile + w;
-#if DN_PRNG_X2
-  // coefficients in pairs: two blocks through the rounds side by side
-#pragma unroll
-  for (int j = 1; j + 1 < T; j += 2) chacha_block2(c[j], c[j + 1], a.key, g * (T - 1) + (j - 1), g * (T - 1) + j);
-  if constexpr ((T - 1) % 2) chacha_block(c[T - 1], a.key, g * (T - 1) + (T - 2));
-#else
-#pragma unroll
-  for (int j = 1; j < T; ++j) chacha_block(c[j], a.key, g * (T - 1) + (j - 1));
-#endif
 #pragma unroll
   for (int j = 1; j < T; ++j) {
     const uint64_t i = g * (T - 1) + (j - 1);
+    chacha_block(c[j], a.key, i);
     c[j][16] = tops[w * (T - 1) + (j - 1)] & kTopMask;
     if (__builtin_expect(prng_rejected(c[j]), 0)) prng_retry(c[j], a.key, i);
     add_small(c[j], 1u);
@@ -173,66 +159,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
   // PRNG: per-wave slice of the tile's top-limb words
   __shared__ uint32_t s_tops[PRNG ? kWavesPerBlock : 1][PRNG ? 256 * (T - 1) : 1];
   uint32_t* tops = s_tops[PRNG ? (threadIdx.x >> 6) : 0];
-  constexpr bool kPrngTile = PRNG && T <= 3;
-  __shared__ uint64_t s_secs[kPrngTile ? kWavesPerBlock : 1][kPrngTile ? 256 : 1];
-  uint64_t* secs = s_secs[kPrngTile ? (threadIdx.x >> 6) : 0];
   for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
-    if constexpr (kPrngTile) {
-      // The tile's secrets are loaded before its top-limb blocks and parked in
-      // LDS: a load issued after a quarter's share stores would wait for them
-      // (loads and stores retire in issue order); the quarters load nothing.
-      uint64_t sec[4];
-      const int64_t* sp = a.sec_u64 + static_cast<uint64_t>(tile) * kTile;  // uniform base
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint64_t e = static_cast<uint64_t>(tile) * kTile + lane + 64u * q;
-        sec[q] = e < a.n_elem ? static_cast<uint64_t>(__builtin_nontemporal_load(sp + lane + 64u * q)) : 0ull;
-      }
-      prng_tile_tops<T>(a, tile, lane, tops);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) secs[lane + 64u * q] = sec[q];  // waits here, before the tile's first store
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t w = lane + 64u * q;
-        const uint64_t e = static_cast<uint64_t>(tile) * kTile + w;
-        if (static_cast<uint32_t>(q) < ws.q0 || static_cast<uint32_t>(q) >= ws.q1 || e >= a.n_elem) continue;
-        uint32_t c[T][kLimbs];
-        prng_coeffs_of<T>(a, tile, w, tops, c);
-        const uint64_t sv = secs[w];
-        c[0][0] = static_cast<uint32_t>(sv);
-        c[0][1] = static_cast<uint32_t>(sv >> 32);
-#pragma unroll
-        for (int i = 2; i < kLimbs; ++i) c[0][i] = 0u;
-        if constexpr (!FOLD) {
-          fd_init<T>(c);
-#pragma unroll 1
-          for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
-            store_reduced<SAUX>(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)),
-                                w, c[0]);
-            fd_step<T>(c);
-          }
-        } else {
-#pragma unroll 1
-          for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
-            const uint32_t x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(xi));
-            uint32_t v[kLimbs];
-            mul_small_add(v, c[T - 1], x, c[T - 2]);
-            if constexpr (T > 2) fold(v);
-#pragma unroll
-            for (int j = T - 3; j >= 0; --j) {
-              mul_small_add(v, x, c[j]);
-              if (j > 0) fold(v);
-            }
-            reduce(v);
-            store_fe_b(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)), w, v);
-          }
-        }
-      }
-      continue;
-    }
     if constexpr (PRNG) prng_tile_tops<T>(a, tile, lane, tops);
 #pragma unroll 1
     for (uint32_t q = ws.q0; q < ws.q1; ++q) {
