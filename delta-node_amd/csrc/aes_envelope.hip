@@ -45,6 +45,11 @@
 #ifndef DN_AES_SDWA
 #define DN_AES_SDWA 1
 #endif
+// DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
+// interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
+#ifndef DN_AES_NB
+#define DN_AES_NB 3
+#endif
 
 namespace dn {
 
@@ -163,10 +168,45 @@ __device__ __forceinline__ void addr_byte(uint32_t& ar, uint32_t s) {
   else asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(ar) : "v"(s));
 }
 
+// a ^ b ^ c in one v_bitop3 (table 0x96); the compiler leaves the round's
+// five-term XORs as four v_xor_b32.  xor3s takes a wave-uniform third operand
+// (a round-key SGPR: VOP3 reads at most one SGPR).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
+
 template <int K, int T>
 __device__ __forceinline__ uint32_t te_sdwa(const AesLds<4>& L, uint32_t s, uint32_t& ar) {
   addr_byte<K>(ar, s);
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&L.tab[0][0][0]) + ar + 128 * (T & 1));
+}
+
+// Final round (SubBytes + ShiftRows + AddRoundKey) through the same address
+// registers as the middle rounds: x_t = Te_t[byte 3 - t of column c + t]
+// holds S at byte 2 (Te0), 1 (Te1), 0 (Te2), 2 (Te3); two v_perm place the
+// four S bytes, one v_bitop3 adds the round key.
+__device__ __forceinline__ void final_round_sdwa(const AesLds<4>& L, const uint32_t st[4], uint32_t (&ar)[4][4],
+                                                 const uint32_t* rk, uint32_t out[4]) {
+  uint32_t x[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    x[c][0] = te_sdwa<3, 0>(L, st[c], ar[c][0]);
+    x[c][1] = te_sdwa<2, 1>(L, st[(c + 1) & 3], ar[c][1]);
+    x[c][2] = te_sdwa<1, 2>(L, st[(c + 2) & 3], ar[c][2]);
+    x[c][3] = te_sdwa<0, 3>(L, st[(c + 3) & 3], ar[c][3]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    out[c] = xor3s(__builtin_amdgcn_perm(x[c][0], x[c][1], 0x06010C0Cu),
+                   __builtin_amdgcn_perm(x[c][2], x[c][3], 0x0C0C0402u), rk[c]);
 }
 
 template <int NR, int NTAB>
@@ -193,15 +233,13 @@ __device__ __forceinline__ void aes_block(const AesLds<NTAB>& L, const uint32_t 
         x[c][3] = te_sdwa<0, 3>(L, st[(c + 3) & 3], ar[c][3]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      s0 = x[0][0] ^ x[0][1] ^ x[0][2] ^ x[0][3] ^ a.rk[4 * r];
-      s1 = x[1][0] ^ x[1][1] ^ x[1][2] ^ x[1][3] ^ a.rk[4 * r + 1];
-      s2 = x[2][0] ^ x[2][1] ^ x[2][2] ^ x[2][3] ^ a.rk[4 * r + 2];
-      s3 = x[3][0] ^ x[3][1] ^ x[3][2] ^ x[3][3] ^ a.rk[4 * r + 3];
+      s0 = xor3s(xor3(x[0][0], x[0][1], x[0][2]), x[0][3], a.rk[4 * r]);
+      s1 = xor3s(xor3(x[1][0], x[1][1], x[1][2]), x[1][3], a.rk[4 * r + 1]);
+      s2 = xor3s(xor3(x[2][0], x[2][1], x[2][2]), x[2][3], a.rk[4 * r + 2]);
+      s3 = xor3s(xor3(x[3][0], x[3][1], x[3][2]), x[3][3], a.rk[4 * r + 3]);
     }
-    s[0] = sub_col(L, lw, s0, s1, s2, s3, a.rk[4 * NR]);
-    s[1] = sub_col(L, lw, s1, s2, s3, s0, a.rk[4 * NR + 1]);
-    s[2] = sub_col(L, lw, s2, s3, s0, s1, a.rk[4 * NR + 2]);
-    s[3] = sub_col(L, lw, s3, s0, s1, s2, a.rk[4 * NR + 3]);
+    const uint32_t st[4] = {s0, s1, s2, s3};
+    final_round_sdwa(L, st, ar, a.rk + 4 * NR, s);
     return;
   }
 #endif
@@ -220,6 +258,53 @@ __device__ __forceinline__ void aes_block(const AesLds<NTAB>& L, const uint32_t 
   s[1] = sub_col(L, lw, s1, s2, s3, s0, a.rk[4 * NR + 1]);
   s[2] = sub_col(L, lw, s2, s3, s0, s1, a.rk[4 * NR + 2]);
   s[3] = sub_col(L, lw, s3, s0, s1, s2, a.rk[4 * NR + 3]);
+}
+
+// NB independent blocks (NTAB == 4, SDWA addressing) with their rounds
+// interleaved: each round issues the 16 lookups of every block back to back,
+// then the XORs, so a wave has 16 NB LDS reads in flight per round instead of
+// 16 (4 waves per SIMD at one 1024-thread workgroup per CU hide too little of
+// one block's read latency).  The 16 address registers are shared by the
+// blocks: a lookup's register is rewritten for the next block after the read
+// that used it has been issued (in order).
+template <int NR, int NB>
+__device__ __forceinline__ void aes_blocks(const AesLds<4>& L, const uint32_t lw[2], const AesArgs& a,
+                                           uint32_t s[NB][4]) {
+#if DN_AES_SDWA
+  uint32_t st[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[b][i] = s[b][i] ^ a.rk[i];
+  uint32_t ar[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ar[c][t] = lw[t >> 1];
+#pragma unroll
+  for (int r = 1; r < NR; ++r) {
+    uint32_t x[NB][4][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        x[b][c][0] = te_sdwa<3, 0>(L, st[b][c], ar[c][0]);
+        x[b][c][1] = te_sdwa<2, 1>(L, st[b][(c + 1) & 3], ar[c][1]);
+        x[b][c][2] = te_sdwa<1, 2>(L, st[b][(c + 2) & 3], ar[c][2]);
+        x[b][c][3] = te_sdwa<0, 3>(L, st[b][(c + 3) & 3], ar[c][3]);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) st[b][c] = xor3s(xor3(x[b][c][0], x[b][c][1], x[b][c][2]), x[b][c][3], a.rk[4 * r + c]);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) final_round_sdwa(L, st[b], ar, a.rk + 4 * NR, s[b]);
+#else
+#pragma unroll
+  for (int b = 0; b < NB; ++b) aes_block<NR>(L, lw, a, s[b]);
+#endif
 }
 
 // Counter block iv + b (mod 2^128) as big-endian words.
@@ -508,13 +593,29 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
     uint32_t W[12];
     shift_raw<3>(R, a.skew, W);
     if (next_whole) load_raw<3>(a.in, a.skew, 48 * gn - 16, R);
+    if constexpr (NTAB == 4 && DN_AES_NB > 1) {
+      uint32_t ks[3][4];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      uint32_t ks[4];
-      ctr_block(a.iv, 3 * g - 1 + j, ks);
-      aes_block<NR>(L, lw, a, ks);
+      for (int j = 0; j < 3; ++j) ctr_block(a.iv, 3 * g - 1 + j, ks[j]);
+      if constexpr (DN_AES_NB == 3) {
+        aes_blocks<NR, 3>(L, lw, a, ks);
+      } else {
+        aes_blocks<NR, 2>(L, lw, a, ks);
+        aes_block<NR>(L, lw, a, ks[2]);
+      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) W[4 * j + i] = __builtin_bswap32(W[4 * j + i]) ^ ks[i];
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) W[4 * j + i] = __builtin_bswap32(W[4 * j + i]) ^ ks[j][i];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        uint32_t ks[4];
+        ctr_block(a.iv, 3 * g - 1 + j, ks);
+        aes_block<NR>(L, lw, a, ks);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) W[4 * j + i] = __builtin_bswap32(W[4 * j + i]) ^ ks[i];
+      }
     }
     uint32_t C[16];
     b64_unit(W, C);
@@ -525,7 +626,15 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
         uint32_t h0, h1, h2, h3;
         hex_word_b64(C[2 * v], h0, h1);
         hex_word_b64(C[2 * v + 1], h2, h3);
+#ifdef DN_AES_DIAG_COALESCED  // timing diagnostic only: lane-contiguous stores, output permuted
+        const uint64_t g0 = g - (threadIdx.x & 63u);  // the wave's first unit
+        if (g0 + 64u < a.units)
+          store4(a.out + 128 * g0 + 1024 * v + 16 * (threadIdx.x & 63u), h0, h1, h2, h3, a.plain != 0u);
+        else
+          store4(o + 16 * v, h0, h1, h2, h3, a.plain != 0u);
+#else
         store4(o + 16 * v, h0, h1, h2, h3, a.plain != 0u);
+#endif
       }
     } else {
       uint8_t* o = a.out + 64 * g;
