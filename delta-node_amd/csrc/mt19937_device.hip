@@ -348,7 +348,14 @@ struct GenArgs {
   uint64_t n_elem;
   int32_t n_shares;
   uint32_t ring;         // ring slots of one wave (2 emission groups; GenRing)
+  uint32_t back;         // even substreams 2 .. S-2 run backward from the next window
 };
+
+// Substream s runs forward from W(s) unless backward generation is on and s
+// is even, not 0 and not the last (then backward from W(s + 1)).
+__host__ __device__ inline bool mt_sub_forward(uint32_t s, uint64_t S, bool back) {
+  return !back || s == 0u || (s & 1u) || s + 1u >= S;
+}
 
 // Raw (untempered) words of a substream pass through an LDS ring of M words
 // (M = two emission groups): stream word p sits at slot (p + delta) mod M,
@@ -452,6 +459,78 @@ __device__ __forceinline__ void ring_init(uint32_t* Rg, const GenRing& g, const 
     Rg[g.o + s] = v;
     if (s < 64u) Rg[g.o + g.M + s] = v;
   }
+}
+
+// ---- backward generation ----------------------------------------------------
+// The word transition is invertible, so one jump window serves two
+// substreams: substream s + 1 forward from W(s + 1) and substream s backward
+// from it (W(s + 1) is the last 624 raw words of substream s).  Only windows
+// of odd s (and of the last substream) are jumped to — half of level B.
+// From word p + 624 = mix(x_p, x_{p+1}, x_{p+397}) with t_p = x_{p+624} ^
+// x_{p+397} = (y >> 1) ^ (y odd ? A : 0), y = (x_p & UP) | (x_{p+1} & LO):
+// A's top bit is set and y >> 1's is clear, so y's low bit is t_p's top bit and
+// y = ((t_p ^ (that bit ? A : 0)) << 1) | bit.  x_p takes its top bit from y_p
+// (bit 30 of t_p, A's bit 30 being clear) and its low 31 bits from y_{p-1}:
+//   x_p = alignbit(bfi(2^30, t_p, t_{p-1} ^ (A & -(t_{p-1} >> 31))), t_{p-1}, 31)
+// — six VALU over words p + 396, p + 397, p + 623 and p + 624.  A word needs
+// none of the 395 words below it, so six 64-word blocks are independent.
+__device__ __forceinline__ uint32_t mt_unmix(uint32_t x396, uint32_t x397, uint32_t x623, uint32_t x624) {
+  const uint32_t t1 = x624 ^ x397, t0 = x623 ^ x396;
+  const uint32_t m0 = static_cast<uint32_t>(static_cast<int32_t>(t0) >> 31);
+  uint32_t u0, up;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(u0) : "v"(m0), "s"(kMtA), "v"(t0));  // (m0 & A) ^ t0
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(up) : "s"(0x40000000u), "v"(t1), "v"(u0));
+  return __builtin_amdgcn_alignbit(up, t0, 31);
+}
+
+// B blocks below ring slot `top` (block i: slots [top - 64 (i + 1), top - 64 i),
+// lane = word), reads first.  Backward substreams use delta = 0 (slot =
+// position mod M).  WRAP: operand slots at or past M wrap (top > M - 624).
+// PART: only slots below `lim` are written (the first block under the window).
+template <int B, bool WRAP, bool PART>
+__device__ __forceinline__ void back_blocks(uint32_t* Rg, uint32_t M, uint32_t top, uint32_t lane, uint32_t lim) {
+  uint32_t q[B], x396[B], x397[B], x623[B], x624[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    q[i] = top - 64u * (i + 1) + lane;
+    if constexpr (WRAP) {
+      auto w = [&](uint32_t s) { return Rg[s >= M ? s - M : s]; };
+      x396[i] = w(q[i] + 396u);
+      x397[i] = w(q[i] + 397u);
+      x623[i] = w(q[i] + 623u);
+      x624[i] = w(q[i] + 624u);
+    } else {
+      const uint32_t* p = Rg + q[i] + 396u;
+      x396[i] = p[0];
+      x397[i] = p[1];
+      x623[i] = p[227];
+      x624[i] = p[228];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every read issued before the first unmix waits
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    const uint32_t v = mt_unmix(x396[i], x397[i], x623[i], x624[i]);
+    if (!PART || q[i] < lim) Rg[q[i]] = v;
+  }
+}
+
+template <int B>
+__device__ __forceinline__ void back_batch(uint32_t* Rg, uint32_t M, uint32_t& top, uint32_t lane) {
+  const uint32_t t0 = __builtin_amdgcn_readfirstlane(top);
+  if (t0 + 624u <= M) back_blocks<B, false, false>(Rg, M, t0, lane, 0u);
+  else back_blocks<B, true, false>(Rg, M, t0, lane, 0u);
+  top = t0 - 64u * B;
+}
+
+// NB blocks down from `top`, as batches of six (one shorter last); a run that
+// ended at slot 0 continues from slot M.
+template <int NB>
+__device__ __forceinline__ void back_run(uint32_t* Rg, uint32_t M, uint32_t& top, uint32_t lane) {
+  if (top == 0u) top = M;
+#pragma unroll
+  for (int k = 0; k + 6 <= NB; k += 6) back_batch<6>(Rg, M, top, lane);
+  if constexpr (NB % 6) back_batch<NB % 6>(Rg, M, top, lane);
 }
 
 // 64 draws of one group (lane = draw c of this substream, raw words 17 c ..
@@ -564,12 +643,16 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   const uint32_t sub = blockIdx.x;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
   const bool fin_wave = sub == a.S;
-  const uint32_t wsel = fin_wave ? static_cast<uint32_t>(a.final_sig) : sub;
+  const bool fwd = fin_wave || mt_sub_forward(sub, a.S, a.back != 0u);
+  const uint32_t sub_words = 17u * static_cast<uint32_t>(a.sub_draws);
+  const uint32_t wsel = fin_wave ? static_cast<uint32_t>(a.final_sig) : fwd ? sub : sub + 1u;
   const uint32_t* win = a.wins + static_cast<uint64_t>(wsel) * kMtN;
   // positions of this substream: word 0 is its first output; the window holds
   // [p_start - 624, p_start) (substream 0: the caller's array, whose words
-  // idx .. 623 are outputs 0 .. 623 - idx)
-  const uint32_t p_start = (sub == 0 && !fin_wave) ? kMtN - a.idx : 0u;
+  // idx .. 623 are outputs 0 .. 623 - idx; a backward substream: its last 624
+  // words, slots M - 624 .. M - 1 since the substream is a whole number of
+  // ring lengths)
+  const uint32_t p_start = (sub == 0 && !fin_wave) ? kMtN - a.idx : fwd ? 0u : sub_words;
   GenRing g;
   g.M = a.ring;
   g.delta = (64u - (p_start & 63u)) & 63u;
@@ -605,6 +688,53 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   const uint64_t qb = k0 / static_cast<uint64_t>(a.tm1);
   const uint32_t rbm = static_cast<uint32_t>(k0 - qb * static_cast<uint64_t>(a.tm1));
   constexpr int kRun = 17 * (T ? T - 1 : 1);  // appends per run = one group's words / 64
+  static_assert(kRun > 10, "a group holds the 640 words under the window");
+  if (!fwd) {
+    // Backward: whole groups, all inside the vector (never the last
+    // substream), last group first; group gi sits in ring half gi % 2
+    // (ngroups is even, so the window is the top of half 1).  First the 16
+    // words under the window (one block, masked), then the group's other
+    // kRun - 10 blocks, then per group: emit it, generate the one below.
+    const uint32_t M = a.ring;
+    back_blocks<1, true, true>(R, M, M - 576u, lane, M - 624u);
+    uint32_t top = M - 640u;
+    back_run<kRun - 10>(R, M, top, lane);
+    wave_sync();
+    if constexpr (T == 0) {
+      for (uint32_t gi = ngroups - 1u;; --gi) {
+        emit_group(a, R + (gi & 1u) * group, qb, rbm, 64u * gi + lane, nloc, lane);
+        if (gi == 0u) break;
+        wave_sync();
+        back_run<kRun>(R, M, top, lane);
+        wave_sync();
+      }
+    } else {
+      // the next (lower) group's secrets loaded before this group's share
+      // stores, into one of two registers by parity (as the forward loop)
+      const uint64_t e0 = qb + lane;
+      auto secret_of = [&](uint32_t gi) {
+        return static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + e0 + 64u * gi));
+      };
+      auto bstep = [&](uint32_t gi, uint64_t cur, uint64_t& nxt) {
+        back_run<kRun>(R, M, top, lane);
+        wave_sync();
+        nxt = secret_of(gi ? gi - 1u : 0u);
+        emit_split<T, SAUX, NS, true>(a, R + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+        wave_sync();
+      };
+      uint64_t secA = secret_of(ngroups - 1u), secB = secret_of(ngroups - 2u);
+      emit_split<T, SAUX, NS, true>(a, R + group, qb + 64u * (ngroups - 1u), lane, secA);
+      wave_sync();
+      for (uint32_t gi = ngroups - 2u;; gi -= 2u) {
+        bstep(gi, secB, secA);
+        if (gi == 0u) break;
+        bstep(gi - 1u, secA, secB);
+        if (gi == 1u) break;
+      }
+      asm volatile("" : : "v"(secA ^ secB));  // no load left in flight at the end
+    }
+    return;
+  }
   // Every run appends exactly one group's words (have = p_start + runs * group
   // with p_start < group), so each run is followed by exactly one emission.
   if constexpr (T == 0) {
@@ -737,8 +867,9 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
 // Levels for windows 1 .. S-1 (s - 1 = 4096 c + 64 a + b; row S holds W_idx;
 // part rows from S + 1) with the jump table of substream length ki:
 // A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a) = C_c(W(1 + 64 a));
-// B: W(base + b) = B_b(W(base)).
-void build_levels(uint64_t S, int ki, Level lv[3]) {
+// B: W(base + b) = B_b(W(base)).  back: only the windows a generation wave
+// starts from (mt_sub_forward: odd s, the last one) — A and C windows are odd.
+void build_levels(uint64_t S, int ki, bool back, Level lv[3]) {
   const uint64_t R = kMtJumpRadix;
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
@@ -765,7 +896,8 @@ void build_levels(uint64_t S, int ki, Level lv[3]) {
     for (uint64_t base = 0; base <= last; base += R) {  // B: per source W(1 + base)
       std::vector<std::pair<int32_t, int32_t>> pd;
       for (uint64_t b = 1; b < R && base + b <= last; ++b)
-        pd.push_back({t0 + kMtRowB + static_cast<int32_t>(b), static_cast<int32_t>(1 + base + b)});
+        if (mt_sub_forward(static_cast<uint32_t>(1 + base + b), S, back))
+          pd.push_back({t0 + kMtRowB + static_cast<int32_t>(b), static_cast<int32_t>(1 + base + b)});
       if (!pd.empty()) srcs.push_back({static_cast<int32_t>(1 + base), pd});
     }
     push_level(lv[2], srcs, prow0);
@@ -778,17 +910,26 @@ void build_levels(uint64_t S, int ki, Level lv[3]) {
 struct MtHost {
   uint64_t S = ~0ull;
   int ki = -1;
+  bool back = false;
   Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
 };
 thread_local MtHost tls_mt;
 
+// Backward generation of the even substreams (on; DN_MT_BACK=0 in the tuning
+// build turns it off for A/B).
+bool mt_back() {
+  const char* e = tune_env("DN_MT_BACK");
+  return !(e && e[0] == '0');
+}
+
 MtHost& mt_levels(uint64_t S, int ki) {
   MtHost& H = tls_mt;
-  if (H.S != S || H.ki != ki) {
+  const bool back = mt_back();
+  if (H.S != S || H.ki != ki || H.back != back) {
     for (auto& l : H.lv) l = Level();
-    build_levels(S, ki, H.lv);
+    build_levels(S, ki, back, H.lv);
     uint64_t nj = 0, nc = 0;
     for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
     H.part_rows = 0;
@@ -806,6 +947,7 @@ MtHost& mt_levels(uint64_t S, int ki) {
     }
     H.S = S;
     H.ki = ki;
+    H.back = back;
   }
   return H;
 }
@@ -971,6 +1113,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   ga.final_pos = fpos;
   ga.final_tf = ftf;
   ga.n_elem = n_elem;
+  ga.back = H.back ? 1u : 0u;
   launch_gen(ga, s);
   err = hipGetLastError();
   if (err != hipSuccess) {

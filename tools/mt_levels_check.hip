@@ -1,9 +1,11 @@
 // mt_levels_check.hip — host check of the MT19937 device draw's jump-job
 // builder (build_levels / push_level in delta-node_amd/csrc/mt19937_device.hip,
 // included here; no GPU needed): for substream counts S up to 300 and the
-// boundary sizes up to 65537, for all three substream lengths, every window
-// 1 .. S-1 is produced exactly once (by a whole jump, or by the XOR of its
-// parts), every source exists before its level, a workgroup's jobs share one
+// boundary sizes up to 65537, for all three substream lengths and both
+// generation modes, every window a generation wave starts from (1 .. S-1, or
+// with backward generation the odd ones and S-1: mt_sub_forward) is produced
+// exactly once (by a whole jump, or by the XOR of its parts) and no other
+// window is, every source exists before its level, a workgroup's jobs share one
 // source and one part (one table), part rows stay within the part-row region
 // and cover the polynomial's words [0, 312) in order.
 // Exit status 1 on any violation.
@@ -18,9 +20,9 @@ uint64_t mt_jump_words() { return 0; } uint64_t mt_jump_max_subs() { return 2621
 void mt_advance_window(const uint32_t*, uint64_t, uint32_t*) {} }
 using namespace dn;
 extern "C" uint64_t dn_m521_vec_bytes(uint64_t n) { return n; }
-int check(uint64_t S, int ki) {
+int check(uint64_t S, int ki, bool back) {
   Level LV[3];
-  build_levels(S, ki, LV);
+  build_levels(S, ki, back, LV);
   std::vector<const Level*> lv = {&LV[0], &LV[1], &LV[2]};
   std::vector<int> known(S + 1 + kPartRows + 8, 0);
   known[0] = 1; known[S] = 1;
@@ -67,8 +69,9 @@ int check(uint64_t S, int ki) {
     if (!partw.empty()) bad++;
     for (size_t i = 0; i < known.size(); ++i) if (known[i] == 2) known[i] = 1;
   }
-  for (uint64_t s = 1; s < S; ++s) if (!known[s]) { bad++; }
-  if (bad) printf("S=%llu ki=%d bad=%d\n", (unsigned long long)S, ki, bad);
+  for (uint64_t s = 1; s < S; ++s)
+    if (!known[s] != !mt_sub_forward(static_cast<uint32_t>(s), S, back)) bad++;
+  if (bad) printf("S=%llu ki=%d back=%d bad=%d\n", (unsigned long long)S, ki, back, bad);
   return bad != 0;
 }
 int main() {
@@ -77,10 +80,11 @@ int main() {
   for (uint64_t S = 1; S < 300; ++S) Ss.push_back(S);
   for (uint64_t S : {511ull, 512ull, 513ull, 1024ull, 1025ull, 2047ull, 2048ull, 2049ull, 4095ull, 4096ull, 4097ull, 4098ull, 5000ull, 8193ull, 16385ull, 20000ull, 65537ull})
     Ss.push_back(S);
-  for (uint64_t S : Ss) for (int ki = 0; ki < 3; ++ki) fails += check(S, ki);
+  for (uint64_t S : Ss)
+    for (int ki = 0; ki < 3; ++ki) fails += check(S, ki, false) + check(S, ki, true);
   // summary for a few sizes
   for (uint64_t S : {2ull, 129ull, 513ull, 2049ull, 4097ull, 16385ull}) {
-    Level L[3]; build_levels(S, 2, L);
+    Level L[3]; build_levels(S, 2, true, L);
     printf("S=%6llu", (unsigned long long)S);
     for (int k = 0; k < 3; ++k) printf("  level %c: W=%d workgroups=%zu combines=%zu", "ACB"[k], L[k].W, L[k].jobs.size() / L[k].W, L[k].comb.size());
     printf("\n");

@@ -128,6 +128,26 @@ __global__ void k_addc(uint32_t* out, uint32_t s) {
   if (r == 0x1234567u) out[0] = r;
 }
 
+
+// encodings: a VOP2 op in its 64-bit VOP3 form, SDWA and DPP forms, bitop3 / bfi
+#define K1(NAME, INSN)                                                   \
+  __global__ void NAME(uint32_t* out, uint32_t s) {                     \
+    uint32_t v[kChains];                                                 \
+    for (int c = 0; c < kChains; ++c) v[c] = threadIdx.x + c;            \
+    BODY(asm volatile(INSN : "+v"(v[c]) : "v"(s)));                     \
+    uint32_t r = 0;                                                      \
+    for (int c = 0; c < kChains; ++c) r ^= v[c];                         \
+    if (r == 0x1234567u) out[0] = r;                                     \
+  }
+K1(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
+K1(k_xor_sdwa, "v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0")
+K1(k_mov_sdwa, "v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2")
+K1(k_add_dpp, "v_add_u32_dpp %0, %1, %0 row_shr:1 bound_ctrl:0")
+K1(k_bitop3, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96")
+K1(k_bfi, "v_bfi_b32 %0, %1, %0, %1")
+K1(k_pk_add, "v_pk_add_u16 %0, %0, %1")
+K1(k_lshl_e32, "v_lshlrev_b32_e32 %0, %1, %0")
+
 template <typename K>
 static void run(const char* name, K k, int ops_per_body) {
   uint32_t* out;
@@ -164,5 +184,13 @@ int main() {
   run("v_lshl_or_b32", k_lshl_or, 1);
   run("v_add3_u32", k_add3, 1);
   run("v_addc_co_u32", k_addc, 1);
+  run("v_xor_b32_e64", k_xor_e64, 1);
+  run("v_xor_b32_sdwa", k_xor_sdwa, 1);
+  run("v_mov_b32_sdwa", k_mov_sdwa, 1);
+  run("v_add_u32_dpp", k_add_dpp, 1);
+  run("v_bitop3_b32", k_bitop3, 1);
+  run("v_bfi_b32", k_bfi, 1);
+  run("v_pk_add_u16", k_pk_add, 1);
+  run("v_lshlrev_b32_e32", k_lshl_e32, 1);
   return 0;
 }
