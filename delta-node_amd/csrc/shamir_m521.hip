@@ -117,16 +117,32 @@ __device__ __forceinline__ void load_secret(const SplitArgs& a, uint32_t tile, u
 // chacha_device.hpp): per tile, the wave first computes the 16 (T-1) blocks
 // holding the tile's top limbs (one block per lane) into its LDS slice, then
 // each lane generates its element's T-1 low blocks in place in c[1..T-1].
-template <int T>
-__device__ __forceinline__ void prng_tile_tops(const SplitArgs& a, uint32_t tile, uint32_t lane, uint32_t* tops) {
+// Tiles whose top-limb blocks one pass computes: 16 (T-1) blocks per tile,
+// one per lane, so T = 2 and 3 take four and two tiles per pass (every lane
+// busy) instead of leaving 48 or 32 lanes idle.  DN_PRNG_TP=0 (variant
+// build): one tile per pass.
+#ifndef DN_PRNG_TP
+#define DN_PRNG_TP 1
+#endif
+__host__ __device__ constexpr int prng_tiles_per_pass(int t) {
+  return (DN_PRNG_TP && 16 * (t - 1) < 64) ? 64 / (16 * (t - 1)) : 1;
+}
+
+// Top-limb blocks of tiles tile0, tile0 + step, ... (TP of them, those below
+// end) into the wave's LDS slice: tile k's at tops + 256 (T-1) k.
+template <int T, int TP>
+__device__ __forceinline__ void prng_tile_tops(const SplitArgs& a, uint32_t tile0, uint32_t step, uint32_t end,
+                                               uint32_t lane, uint32_t* tops) {
   constexpr uint32_t kBlocks = 16u * (T - 1);  // 256 (T-1) top words per tile
-  const uint64_t g0 = a.elem_offset + static_cast<uint64_t>(tile) * kTile;
-  const uint64_t b0 = kTopDomain + g0 * (T - 1) / 16u;
-  __builtin_amdgcn_wave_barrier();  // previous tile's reads are done
+  __builtin_amdgcn_wave_barrier();  // previous tiles' reads are done
 #pragma unroll 1
-  for (uint32_t b = lane; b < kBlocks; b += 64u) {
+  for (uint32_t b = lane; b < kBlocks * TP; b += 64u) {
+    const uint32_t k = b / kBlocks, bb = b - k * kBlocks;
+    const uint32_t tile = tile0 + k * step;
+    if (tile >= end) continue;
+    const uint64_t g0 = a.elem_offset + static_cast<uint64_t>(tile) * kTile;
     uint32_t x[16];
-    chacha_block(x, a.key, b0 + b);
+    chacha_block(x, a.key, kTopDomain + g0 * (T - 1) / 16u + bb);
 #pragma unroll
     for (int i = 0; i < 16; ++i) tops[b * 16u + i] = x[i];
   }
@@ -151,16 +167,21 @@ __device__ __forceinline__ void prng_coeffs_of(const SplitArgs& a, uint32_t tile
 
 constexpr int kMaxPrngT = 8;
 
-template <int T, bool FE_SECRET, bool FOLD, bool PRNG = false, int SAUX = kNt>
-__global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
+template <int T, bool FE_SECRET, bool FOLD, bool PRNG, int SAUX>
+__device__ __forceinline__ void split_body(const SplitArgs& a) {
   const uint32_t lane = threadIdx.x & 63u;
   const WaveSched ws = wave_sched(a.tile_map, a.ntiles);
   static_assert(!PRNG || (T >= 2 && !FE_SECRET), "PRNG coefficients: u64 secrets, t >= 2");
-  // PRNG: per-wave slice of the tile's top-limb words
-  __shared__ uint32_t s_tops[PRNG ? kWavesPerBlock : 1][PRNG ? 256 * (T - 1) : 1];
-  uint32_t* tops = s_tops[PRNG ? (threadIdx.x >> 6) : 0];
-  for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
-    if constexpr (PRNG) prng_tile_tops<T>(a, tile, lane, tops);
+  // PRNG: per-wave slice of the top-limb words of TP tiles
+  constexpr int TP = PRNG ? prng_tiles_per_pass(T) : 1;
+  __shared__ uint32_t s_tops[PRNG ? kWavesPerBlock : 1][PRNG ? 256 * (T - 1) * TP : 1];
+  uint32_t* tops = s_tops[PRNG ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0];
+  for (uint32_t tile0 = ws.first; tile0 < ws.end; tile0 += ws.step * TP) {
+    if constexpr (PRNG) prng_tile_tops<T, TP>(a, tile0, ws.step, ws.end, lane, tops);
+#pragma unroll 1
+    for (int k = 0; k < TP; ++k) {
+    const uint32_t tile = tile0 + static_cast<uint32_t>(k) * ws.step;
+    if (tile >= ws.end) break;
 #pragma unroll 1
     for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
@@ -168,7 +189,7 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
       if (e >= a.n_elem) break;
       uint32_t c[T][kLimbs];
       if constexpr (PRNG) {
-        prng_coeffs_of<T>(a, tile, w, tops, c);
+        prng_coeffs_of<T>(a, tile, w, tops + 256u * (T - 1) * static_cast<uint32_t>(k), c);
       } else {
 #pragma unroll
         for (int j = 1; j < T; ++j)
@@ -206,7 +227,24 @@ __global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
         }
       }
     }
+    }
   }
+}
+
+template <int T, bool FE_SECRET, bool FOLD, bool PRNG = false, int SAUX = kNt>
+__global__ void __launch_bounds__(kBlock) split_kernel(const SplitArgs a) {
+  split_body<T, FE_SECRET, FOLD, PRNG, SAUX>(a);
+}
+
+// The device-PRNG split, register-limited to DN_PRNG_WAVES waves per SIMD
+// (80 VGPRs at 6): its ChaCha rounds are dependent VALU chains that need the
+// waves to hide their latency.
+#ifndef DN_PRNG_WAVES
+#define DN_PRNG_WAVES 6
+#endif
+template <int T, bool FOLD>
+__global__ void __launch_bounds__(kBlock, DN_PRNG_WAVES) split_prng_kernel(const SplitArgs a) {
+  split_body<T, false, FOLD, true, kNt>(a);
 }
 
 // ---- wide-access difference-table split ------------------------------------
@@ -398,20 +436,26 @@ template <int T>
 __global__ void __launch_bounds__(kBlock) prng_coeffs_kernel(const SplitArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const WaveSched ws = wave_sched(a.tile_map, a.ntiles);
-  __shared__ uint32_t s_tops[kWavesPerBlock][256 * (T - 1)];
-  uint32_t* tops = s_tops[threadIdx.x >> 6];
-  for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
-    prng_tile_tops<T>(a, tile, lane, tops);
+  constexpr int TP = prng_tiles_per_pass(T);
+  __shared__ uint32_t s_tops[kWavesPerBlock][256 * (T - 1) * TP];
+  uint32_t* tops = s_tops[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+  for (uint32_t tile0 = ws.first; tile0 < ws.end; tile0 += ws.step * TP) {
+    prng_tile_tops<T, TP>(a, tile0, ws.step, ws.end, lane, tops);
 #pragma unroll 1
-    for (uint32_t q = ws.q0; q < ws.q1; ++q) {
-      const uint32_t w = lane + 64u * q;
-      if (static_cast<uint64_t>(tile) * kTile + w >= a.n_elem) break;
-      uint32_t c[T][kLimbs];
-      prng_coeffs_of<T>(a, tile, w, tops, c);
+    for (int k = 0; k < TP; ++k) {
+      const uint32_t tile = tile0 + static_cast<uint32_t>(k) * ws.step;
+      if (tile >= ws.end) break;
+#pragma unroll 1
+      for (uint32_t q = ws.q0; q < ws.q1; ++q) {
+        const uint32_t w = lane + 64u * q;
+        if (static_cast<uint64_t>(tile) * kTile + w >= a.n_elem) break;
+        uint32_t c[T][kLimbs];
+        prng_coeffs_of<T>(a, tile, w, tops + 256u * (T - 1) * static_cast<uint32_t>(k), c);
 #pragma unroll
-      for (int j = 1; j < T; ++j)
-        store_fe_b(tile_rsrc(tile_base(const_cast<uint8_t*>(a.coeffs) + static_cast<uint64_t>(j - 1) * a.coeff_stride,
-                                       tile)), w, c[j]);
+        for (int j = 1; j < T; ++j)
+          store_fe_b(tile_rsrc(tile_base(const_cast<uint8_t*>(a.coeffs) + static_cast<uint64_t>(j - 1) * a.coeff_stride,
+                                         tile)), w, c[j]);
+      }
     }
   }
 }
@@ -640,13 +684,13 @@ static bool launch_split_wide(int t, dim3 g, hipStream_t s, const SplitArgs& a) 
 template <bool FOLD>
 static void launch_split_prng(int t, dim3 g, hipStream_t s, const SplitArgs& a) {
   switch (t) {
-    case 2: hipLaunchKernelGGL((split_kernel<2, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((split_kernel<3, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((split_kernel<4, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
-    case 5: hipLaunchKernelGGL((split_kernel<5, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
-    case 6: hipLaunchKernelGGL((split_kernel<6, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
-    case 7: hipLaunchKernelGGL((split_kernel<7, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
-    case 8: hipLaunchKernelGGL((split_kernel<8, false, FOLD, true>), g, dim3(kBlock), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((split_prng_kernel<2, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((split_prng_kernel<3, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((split_prng_kernel<4, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((split_prng_kernel<5, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((split_prng_kernel<6, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((split_prng_kernel<7, FOLD>), g, dim3(kBlock), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((split_prng_kernel<8, FOLD>), g, dim3(kBlock), 0, s, a); break;
     default: break;
   }
 }
@@ -701,7 +745,9 @@ static int split_common(SplitArgs a, int threshold, int n_shares, void* stream, 
   const char* hz = tune_env("DN_SPLIT_HORNER");
   const bool fold_each = fd_needs_fold(threshold, n_shares) || (hz && hz[0] == '1');
   const bool per_cu = !prng && !fold_each && threshold <= 8;  // the memory-bound difference-table kernels
-  const dim3 g(grid_for(a.ntiles, per_cu));
+  // a PRNG wave takes its tiles prng_tiles_per_pass at a time
+  const uint64_t tp = prng ? static_cast<uint64_t>(prng_tiles_per_pass(threshold)) : 1u;
+  const dim3 g(grid_for((a.ntiles + tp - 1) / tp, per_cu));
   a.tile_map = tile_map_for(static_cast<int>(g.x), !prng);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (prng && threshold > 1) {
@@ -760,7 +806,8 @@ extern "C" int dn_m521_prng_coeffs(const uint32_t* key, uint64_t nonce, int roun
   a.ntiles = (n_elem + kTile - 1) / kTile;
   a.vec_bytes = a.ntiles * kTileBytes;
   a.coeff_stride = a.vec_bytes;
-  const dim3 g(grid_for(a.ntiles));
+  const uint64_t tp = static_cast<uint64_t>(prng_tiles_per_pass(tm1 + 1));
+  const dim3 g(grid_for((a.ntiles + tp - 1) / tp));
   a.tile_map = tile_map_for(static_cast<int>(g.x), false);
   launch_prng_coeffs(tm1 + 1, g, static_cast<hipStream_t>(stream), a);
   return check_launch("dn_m521_prng_coeffs");
