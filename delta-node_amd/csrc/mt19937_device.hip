@@ -349,12 +349,28 @@ struct GenArgs {
   int32_t n_shares;
   uint32_t ring;         // ring slots of one wave (2 emission groups; GenRing)
   uint32_t back;         // even substreams 2 .. S-2 run backward from the next window
+  uint32_t probe;        // tuning build only (DN_MT_PROBE): 1 skip emissions, 2 skip generation
 };
 
-// Substream s runs forward from W(s) unless backward generation is on and s
-// is even, not 0 and not the last (then backward from W(s + 1)).
-__host__ __device__ inline bool mt_sub_forward(uint32_t s, uint64_t S, bool back) {
+// DN_MT_PROBE (tuning build): time the generation and the emission apart.
+#ifdef DN_TUNING
+#define DN_PROBE_SKIP(a, bit) if (!((a).probe & (bit)))
+#else
+#define DN_PROBE_SKIP(a, bit)
+#endif
+
+// Substream s runs forward from W(s) unless backward generation is on
+// (back = 1) and s is even, not 0 and not the last (then backward from
+// W(s + 1)).  back = 2 (tuning build, DN_MT_BACK=2: a probe of the backward
+// generation rate) runs every substream but the first and the last backward.
+__host__ __device__ inline bool mt_sub_forward(uint32_t s, uint64_t S, int back) {
+  if (back == 2) return s == 0u || s + 1u >= S;
   return !back || s == 0u || (s & 1u) || s + 1u >= S;
+}
+
+// W(s) is jumped to when substream s starts from it or substream s - 1 ends on it.
+__host__ __device__ inline bool mt_window_needed(uint32_t s, uint64_t S, int back) {
+  return mt_sub_forward(s, S, back) || !mt_sub_forward(s - 1u, S, back);
 }
 
 // Raw (untempered) words of a substream pass through an LDS ring of M words
@@ -567,18 +583,12 @@ __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb,
 // them: raw words 17 ((t-1) lane + j - 1) .. + 16 of the group for
 // coefficient j), their int64 secrets, and the split of split_kernel<T,
 // false, false>: the forward-difference table stored share by share.
-template <int T, int SAUX, int NS, bool WHOLE>
-__device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t ebase, uint32_t lane,
-                                           uint64_t s) {
+// The group's coefficients (ring words of this lane's element, tempered, +1,
+// rejection flagged) and secret s into the difference table c (fd_init).
+template <int T>
+__device__ __forceinline__ void emit_prepare(const GenArgs& a, const uint32_t* rb, uint32_t lane, uint64_t s,
+                                             uint32_t (&c)[T][kLimbs]) {
   constexpr int TM1 = T - 1;
-  // ebase (the group's first element) is wave-uniform and a multiple of 64, so
-  // the group's 64 elements share one tile: its index is a scalar and every
-  // share store takes the tile's buffer descriptor from SGPRs (no per-lane
-  // descriptor, no waterfall loop around the stores)
-  const uint32_t tile = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ebase >> 8));
-  const uint64_t e = ebase + lane;
-  if (!WHOLE && e >= a.n_elem) return;  // WHOLE: every element of the group is in the vector
-  uint32_t c[T][kLimbs];
   const uint32_t* w = rb + 17u * TM1 * lane;
   if constexpr (TM1 % 2 == 0) {
     // an element's 17 (t-1) words start at an even word: 8-B reads, and with
@@ -616,6 +626,20 @@ __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb,
 #pragma unroll
   for (int i = 2; i < kLimbs; ++i) c[0][i] = 0u;
   fd_init<T>(c);
+}
+
+template <int T, int SAUX, int NS, bool WHOLE>
+__device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t ebase, uint32_t lane,
+                                           uint64_t s) {
+  // ebase (the group's first element) is wave-uniform and a multiple of 64, so
+  // the group's 64 elements share one tile: its index is a scalar and every
+  // share store takes the tile's buffer descriptor from SGPRs (no per-lane
+  // descriptor, no waterfall loop around the stores)
+  const uint32_t tile = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(ebase >> 8));
+  const uint64_t e = ebase + lane;
+  if (!WHOLE && e >= a.n_elem) return;  // WHOLE: every element of the group is in the vector
+  uint32_t c[T][kLimbs];
+  emit_prepare<T>(a, rb, lane, s, c);
   const uint32_t wl = static_cast<uint32_t>(e & 255u);
   if constexpr (NS > 0) {
 #pragma unroll
@@ -643,7 +667,7 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   const uint32_t sub = blockIdx.x;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
   const bool fin_wave = sub == a.S;
-  const bool fwd = fin_wave || mt_sub_forward(sub, a.S, a.back != 0u);
+  const bool fwd = fin_wave || mt_sub_forward(sub, a.S, static_cast<int>(a.back));
   const uint32_t sub_words = 17u * static_cast<uint32_t>(a.sub_draws);
   const uint32_t wsel = fin_wave ? static_cast<uint32_t>(a.final_sig) : fwd ? sub : sub + 1u;
   const uint32_t* win = a.wins + static_cast<uint64_t>(wsel) * kMtN;
@@ -739,9 +763,9 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   // with p_start < group), so each run is followed by exactly one emission.
   if constexpr (T == 0) {
     for (uint32_t done = 0; done < ngroups; ++done) {
-      ring_run<kRun>(R, g, slot, lane);
+      DN_PROBE_SKIP(a, 2u) ring_run<kRun>(R, g, slot, lane);
       wave_sync();
-      emit_group(a, R + g.o + g.delta + (done & 1u) * group, qb, rbm, 64u * done + lane, nloc, lane);
+      DN_PROBE_SKIP(a, 1u) emit_group(a, R + g.o + g.delta + (done & 1u) * group, qb, rbm, 64u * done + lane, nloc, lane);
       wave_sync();
     }
   } else {
@@ -765,10 +789,10 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
     const uint64_t rem = a.n_elem - qb;  // elements from this substream's first one to the vector's end
     const uint32_t nfull = rem >= 64ull * ngroups ? ngroups : static_cast<uint32_t>(rem / 64u);
     auto step = [&](uint32_t gi, uint64_t cur, uint64_t& nxt) {
-      ring_run<kRun>(R, g, slot, lane);
+      DN_PROBE_SKIP(a, 2u) ring_run<kRun>(R, g, slot, lane);
       wave_sync();
       nxt = secret_of(gi + 1u);
-      emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+      DN_PROBE_SKIP(a, 1u) emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
       wave_sync();
     };
     uint64_t secA = secret_of(0), secB = 0;
@@ -869,7 +893,7 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
 // A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a) = C_c(W(1 + 64 a));
 // B: W(base + b) = B_b(W(base)).  back: only the windows a generation wave
 // starts from (mt_sub_forward: odd s, the last one) — A and C windows are odd.
-void build_levels(uint64_t S, int ki, bool back, Level lv[3]) {
+void build_levels(uint64_t S, int ki, int back, Level lv[3]) {
   const uint64_t R = kMtJumpRadix;
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
@@ -896,7 +920,7 @@ void build_levels(uint64_t S, int ki, bool back, Level lv[3]) {
     for (uint64_t base = 0; base <= last; base += R) {  // B: per source W(1 + base)
       std::vector<std::pair<int32_t, int32_t>> pd;
       for (uint64_t b = 1; b < R && base + b <= last; ++b)
-        if (mt_sub_forward(static_cast<uint32_t>(1 + base + b), S, back))
+        if (mt_window_needed(static_cast<uint32_t>(1 + base + b), S, back))
           pd.push_back({t0 + kMtRowB + static_cast<int32_t>(b), static_cast<int32_t>(1 + base + b)});
       if (!pd.empty()) srcs.push_back({static_cast<int32_t>(1 + base), pd});
     }
@@ -910,7 +934,7 @@ void build_levels(uint64_t S, int ki, bool back, Level lv[3]) {
 struct MtHost {
   uint64_t S = ~0ull;
   int ki = -1;
-  bool back = false;
+  int back = 0;
   Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
@@ -919,14 +943,14 @@ thread_local MtHost tls_mt;
 
 // Backward generation of the even substreams (on; DN_MT_BACK=0 in the tuning
 // build turns it off for A/B).
-bool mt_back() {
+int mt_back() {
   const char* e = tune_env("DN_MT_BACK");
-  return !(e && e[0] == '0');
+  return e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1) : 1;
 }
 
 MtHost& mt_levels(uint64_t S, int ki) {
   MtHost& H = tls_mt;
-  const bool back = mt_back();
+  const int back = mt_back();
   if (H.S != S || H.ki != ki || H.back != back) {
     for (auto& l : H.lv) l = Level();
     build_levels(S, ki, back, H.lv);
@@ -1113,7 +1137,9 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   ga.final_pos = fpos;
   ga.final_tf = ftf;
   ga.n_elem = n_elem;
-  ga.back = H.back ? 1u : 0u;
+  ga.back = static_cast<uint32_t>(H.back);
+  const char* pr = tune_env("DN_MT_PROBE");
+  ga.probe = pr ? static_cast<uint32_t>(std::atoi(pr)) : 0u;
   launch_gen(ga, s);
   err = hipGetLastError();
   if (err != hipSuccess) {

@@ -20,7 +20,7 @@ uint64_t mt_jump_words() { return 0; } uint64_t mt_jump_max_subs() { return 2621
 void mt_advance_window(const uint32_t*, uint64_t, uint32_t*) {} }
 using namespace dn;
 extern "C" uint64_t dn_m521_vec_bytes(uint64_t n) { return n; }
-int check(uint64_t S, int ki, bool back) {
+int check(uint64_t S, int ki, int back) {
   Level LV[3];
   build_levels(S, ki, back, LV);
   std::vector<const Level*> lv = {&LV[0], &LV[1], &LV[2]};
@@ -81,10 +81,10 @@ int main() {
   for (uint64_t S : {511ull, 512ull, 513ull, 1024ull, 1025ull, 2047ull, 2048ull, 2049ull, 4095ull, 4096ull, 4097ull, 4098ull, 5000ull, 8193ull, 16385ull, 20000ull, 65537ull})
     Ss.push_back(S);
   for (uint64_t S : Ss)
-    for (int ki = 0; ki < 3; ++ki) fails += check(S, ki, false) + check(S, ki, true);
+    for (int ki = 0; ki < 3; ++ki) fails += check(S, ki, 0) + check(S, ki, 1);
   // summary for a few sizes
   for (uint64_t S : {2ull, 129ull, 513ull, 2049ull, 4097ull, 16385ull}) {
-    Level L[3]; build_levels(S, 2, true, L);
+    Level L[3]; build_levels(S, 2, 1, L);
     printf("S=%6llu", (unsigned long long)S);
     for (int k = 0; k < 3; ++k) printf("  level %c: W=%d workgroups=%zu combines=%zu", "ACB"[k], L[k].W, L[k].jobs.size() / L[k].W, L[k].comb.size());
     printf("\n");
