@@ -358,15 +358,16 @@ def envelope_row(recs, reps: int, s, e) -> dict:
     # events on its stream, best of 3 rounds of `reps` launches
     import ctypes as _ct
 
+    from delta_node.crypto.aes import aes as _aes_mod
     from delta_node.crypto.shamir import _native as _cn
 
-    AL = aes._lib()
+    AL = _aes_mod._lib()
     kbuf = torch.empty(16 + int(AL.dn_aes_encrypt_len(n, 1)), dtype=torch.uint8, device=recs.device)
     stream = torch.cuda.current_stream()
 
     def k_enc():
         _cn.check(AL.dn_aes_encrypt(key, len(key), nonce, recs.data_ptr(), n, kbuf.data_ptr() + 16, 1,
-                                    _ct.c_void_p(stream.cuda_stream)))
+                                    stream.cuda_stream))
 
     kern = []
     for _ in range(3):
