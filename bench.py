@@ -752,6 +752,8 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
     # smaller vectors take shorter MT substreams (2^10 / 2^12 / 2^14 draws: dn_mt19937_split_device)
     by_size = {}
     for lg in (12, 16, 20, 22):
+        if lg > log2n:
+            break
         m = 1 << lg
         ss = shamir.SecretShare(3)
         ss.random.seed(lg)

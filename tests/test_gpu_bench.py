@@ -53,3 +53,24 @@ def test_bench_under_launcher_world1_rccl():
     assert line["n_gpus"] == 1 and line["parity"]["all_ranks_ok"] is True
     assert line["config4"]["allgather"]["blocks_equal"] is True
     assert line["config4"]["allgather"]["all_ranks_ok"] is True
+
+
+def test_bench_rows_small():
+    """The one-GPU bench with every §8(f) row on, at 2^18 elements: each row's
+    code runs (a row that raises fails the driver's bench line) and its parity
+    flags hold."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--log2n", "18", "--steps", "2",
+                        "--warmup", "1", "--placements", "2", "--config4", "0", "--config5", "0",
+                        "--cpu-budget", "0"],
+                       capture_output=True, text=True, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["parity"]["all_ranks_ok"] is True
+    rows = line["rows"]
+    for k in ("share_codec", "share_envelope", "split_prng", "member_sum", "mask_masking", "draw_split", "byte_api"):
+        assert k in rows, k
+    assert rows["share_codec"]["roundtrip_equal"] and rows["share_codec"]["kernels_equal_api"]
+    env_row = rows["share_envelope"]
+    assert env_row["roundtrip_equal"] and env_row["oracle_prefix_equal"] and env_row["encrypt_kernel_equal_api"]
+    assert rows["draw_split"]["equal_draw_then_split_and_state"]
