@@ -57,6 +57,20 @@ def roof(bound: str, achieved: float, note: str) -> dict:
 FE_BYTES = 66           # ceil(521 / 8): one field element in the tiled layout
 
 
+def warm(fn, seconds: float = 0.15) -> None:
+    """Run fn back to back for `seconds` of wall time (at least 3 calls): the
+    GPU clock ramps up over tens of milliseconds of sustained work after an
+    idle stretch, and the VALU-heavy rows are timed at the steady clock."""
+    t0 = time.perf_counter()
+    k = 0
+    while k < 3 or time.perf_counter() - t0 < seconds:
+        fn()
+        k += 1
+        if k % 4 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+
+
 def secrets_int64(seed: int, n: int) -> np.ndarray:
     rng = np.random.default_rng(seed)
     return rng.integers(-(1 << 63), (1 << 63) - 1, size=n, endpoint=True, dtype=np.int64)
@@ -370,8 +384,8 @@ def envelope_row(recs, reps: int, s, e) -> dict:
                                     stream.cuda_stream))
 
     kern = []
+    warm(k_enc)
     for _ in range(3):
-        k_enc()
         s.record(stream)
         for _ in range(reps):
             k_enc()
@@ -392,7 +406,7 @@ def envelope_row(recs, reps: int, s, e) -> dict:
            "encrypt_kernel_ms": enc_kernel_ms, "encrypt_kernel_equal_api": kernel_equal,
            "timing": "encrypt_ms / decrypt_ms: the Python API calls (output allocation, decrypt's length "
                      "read-back), mean of one round; encrypt_kernel_ms: dn_aes_encrypt on a preallocated "
-                     "buffer, best of 3 rounds; the rooflines use the kernel time",
+                     "buffer, >= 0.15 s warm-up, best of 3 rounds; the rooflines use the kernel time",
            "encrypt_plaintext_GBps": n / (enc_ms * 1e-3) / 1e9, "decrypt_plaintext_GBps": n / (dec_ms * 1e-3) / 1e9,
            "roofline_lds": roof("lds", lds_bytes / (enc_kernel_ms * 1e-3) / 1e9,
                                 "14 rounds x 16 Te lookups x 4 B per 16-byte block (encrypt kernel)"),
@@ -603,12 +617,10 @@ def rows_bench(dev, log2n: int) -> dict:
     for rounds in (20, 8):
         # The rows before this one end in host-only work (the CPU baselines), and
         # the GPU clock falls while it idles: the VALU-heavy ChaCha20 split then
-        # reads ~20 % slow for its first few milliseconds (scripts/prng_row_probe.py,
-        # profiles/r03/ab/prng_clock/).  So: three warm-up calls, then the best of
-        # three rounds of `reps` launches (each round's mean is reported too).
-        for _ in range(3):
-            _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, sh, n, 3, 5)
-        torch.cuda.synchronize()
+        # reads ~20 % slow for its first tens of milliseconds (scripts/prng_row_probe.py,
+        # profiles/r03/ab/prng_clock/).  So: `warm` (>= 150 ms of the same call),
+        # then the best of three rounds of `reps` launches (each round's mean too).
+        warm(lambda: _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, sh, n, 3, 5))
         rms = []
         for _ in range(3):
             s.record()
@@ -737,6 +749,8 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
     out = torch.empty((5, field.vec_bytes(n)), dtype=torch.uint8, device=dev)
     fused, unfused = [], []
     ok = True
+    wss = shamir.SecretShare(3)
+    warm(lambda: wss.make_shares_vec(sec, 5, out=out))
     for r in range(reps + 1):
         a, b = shamir.SecretShare(3), shamir.SecretShare(3)
         a.random.seed(77 + r)

@@ -111,7 +111,7 @@ struct CombineJob {
 };
 
 struct JumpArgs {
-  uint32_t* wins;  // [S + 1][624]: window s at row s, the caller's window advanced idx words at row S
+  uint32_t* wins;  // window s at row s (row 0 the caller's array), the caller's window advanced idx words at row -1
   const JumpJob* jobs;
   uint32_t njobs;
 };
@@ -241,7 +241,7 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   // the workgroup's jobs share the source and lo (one table; job j0 is never padding)
   const int32_t lo = __builtin_amdgcn_readfirstlane(a.jobs[j0].span) & 0xffff;
   const int32_t hi = __builtin_amdgcn_readfirstlane(jp->span) >> 16;
-  const uint32_t* src = a.wins + static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(a.jobs[j0].src)) * kMtN;
+  const uint32_t* src = a.wins + static_cast<int64_t>(__builtin_amdgcn_readfirstlane(a.jobs[j0].src)) * kMtN;
   if (lo == 0) {
     // the source stream: words 0..623 of W, then 63 more (each from words <= 459 of W)
     for (uint32_t i = tid; i < kMtN; i += 64u * W) ext[i] = src[i];
@@ -861,7 +861,10 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
   size_t n = 0, most = 0;  // jumps, and the most of one source
   for (auto& sp : srcs) n += sp.second.size(), most = std::max(most, sp.second.size());
   if (n == 0) return;
-  const int P = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kMaxParts, kPartRows / n)));
+  int P = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kMaxParts, kPartRows / n)));
+  // DN_MT_PARTS_B (tuning build): the part count of levels of 256 jumps or more
+  const char* pb = n >= 256 ? tune_env("DN_MT_PARTS_B") : nullptr;
+  if (pb && std::atoi(pb) >= 1) P = std::min(kMaxParts, std::atoi(pb));
   const size_t per = std::min<size_t>(kJumpWaves, std::max<size_t>(2, (n * P + 255) / 256));
   L.W = std::min(per, most) > 8 ? 16 : 8;
   if (P == 1) {
@@ -903,7 +906,7 @@ void build_levels(uint64_t S, int ki, int back, Level lv[3]) {
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t a = 0; a <= last / R && a < R; ++a)
       pd.push_back({t0 + kMtRowA + static_cast<int32_t>(a), static_cast<int32_t>(1 + R * a)});
-    push_level(lv[0], {{static_cast<int32_t>(S), pd}}, prow0);
+    push_level(lv[0], {{-1, pd}}, prow0);  // source: W_idx, the row before row 0
   }
   {
     std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>> srcs;
@@ -935,6 +938,7 @@ struct MtHost {
   uint64_t S = ~0ull;
   int ki = -1;
   int back = 0;
+  int parts_b = 0;  // tuning build: DN_MT_PARTS_B the levels were built with
   Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
@@ -951,7 +955,9 @@ int mt_back() {
 MtHost& mt_levels(uint64_t S, int ki) {
   MtHost& H = tls_mt;
   const int back = mt_back();
-  if (H.S != S || H.ki != ki || H.back != back) {
+  const char* pb = tune_env("DN_MT_PARTS_B");
+  const int parts_b = pb ? std::atoi(pb) : 0;
+  if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b) {
     for (auto& l : H.lv) l = Level();
     build_levels(S, ki, back, H.lv);
     uint64_t nj = 0, nc = 0;
@@ -972,6 +978,7 @@ MtHost& mt_levels(uint64_t S, int ki) {
     H.S = S;
     H.ki = ki;
     H.back = back;
+    H.parts_b = parts_b;
   }
   return H;
 }
@@ -1026,6 +1033,9 @@ struct PinLease {
 
 constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
 
+// words the job tables take in the scratch, rounded up to 256 B
+inline uint64_t mt_jobs_pad(const MtHost& H) { return (H.jobs.size() + 63) / 64 * 64; }
+
 }  // namespace
 }  // namespace dn
 
@@ -1036,7 +1046,7 @@ extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
   const uint64_t S = ncoef ? mt_subs(ncoef) : 0;
   if (!S) return kHead + kMtN * 4;
   const MtHost& H = mt_levels(S, mt_sub_len(ncoef));
-  return kHead + (S + 1 + H.part_rows) * kMtN * 4 + H.jobs.size() * 4;
+  return kHead + mt_jobs_pad(H) * 4 + (1 + S + 1 + H.part_rows) * kMtN * 4;
 }
 
 namespace dn {
@@ -1077,32 +1087,31 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     fidx = static_cast<int32_t>(m_end - kMtN * (q - 1));
   }
 
-  // scratch: head (flag at 0, final array at 256) | windows 0..S (row 0 the
-  // caller's array, row S that array advanced idx words) | part rows (split
-  // levels) | jump jobs | combine jobs.  Three copies from the pinned
-  // staging buffer [zeroed head, row 0 | row S | jobs]; the head comes back
-  // into its tail.
+  // scratch: head (flag at 0, final array at 256) | jump jobs, combine jobs
+  // (padded to 256 B) | W_idx (the caller's array advanced idx words: window
+  // "-1", the level-A source) | windows 0..S (row 0 the caller's array; row S
+  // unused) | part rows (split levels).  Everything the GPU needs from the host
+  // is the prefix head .. row 0: ONE copy from the pinned staging buffer,
+  // which holds that prefix and, in its tail, the head read back at the end.
   const int ki = mt_sub_len(ncoef);
   MtHost& H = mt_levels(S, ki);
   const Level* lv = H.lv;
   const uint64_t njobs = lv[0].jobs.size() + lv[1].jobs.size() + lv[2].jobs.size();
-  const size_t w1 = kHead / 4 + kMtN, w2 = kMtN, w3 = H.jobs.size(), wh = 256 / 4 + kMtN;
-  PinLease lease(w1 + w2 + w3 + wh);  // idle again once this call has synchronised its stream
+  const size_t wj = mt_jobs_pad(H), wpre = kHead / 4 + wj + 2 * kMtN, wh = 256 / 4 + kMtN;
+  PinLease lease(wpre + wh);  // idle again once this call has synchronised its stream
   uint32_t* pin = lease.p;
   if (!pin) return set_error(DN_ERR_HIP, "%s: pinned staging buffer", name);
-  uint32_t *st1 = pin, *st2 = pin + w1, *st3 = st2 + w2, *head = st3 + w3;
-  std::memset(st1, 0, kHead);
-  std::memcpy(st1 + kHead / 4, mt_state, kMtN * 4);
-  mt_advance_window(mt_state, static_cast<uint64_t>(idx), st2);
-  if (w3) std::memcpy(st3, H.jobs.data(), w3 * 4);
+  uint32_t *stj = pin + kHead / 4, *stw = stj + wj, *head = pin + wpre;
+  std::memset(pin, 0, kHead);
+  if (!H.jobs.empty()) std::memcpy(stj, H.jobs.data(), H.jobs.size() * 4);
+  mt_advance_window(mt_state, static_cast<uint64_t>(idx), stw);  // W_idx
+  std::memcpy(stw + kMtN, mt_state, kMtN * 4);                    // row 0
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
-  uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead);
-  JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead + (S + 1 + H.part_rows) * kMtN * 4);
+  JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead);
   CombineJob* dcomb = reinterpret_cast<CombineJob*>(djobs + njobs);
-  hipError_t err = hipMemcpyAsync(sc, st1, w1 * 4, hipMemcpyHostToDevice, s);
-  if (err == hipSuccess) err = hipMemcpyAsync(dwin + S * kMtN, st2, w2 * 4, hipMemcpyHostToDevice, s);
-  if (err == hipSuccess && w3) err = hipMemcpyAsync(djobs, st3, w3 * 4, hipMemcpyHostToDevice, s);
+  uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead) + wj + kMtN;  // row 0
+  hipError_t err = hipMemcpyAsync(sc, pin, wpre * 4, hipMemcpyHostToDevice, s);
   if (err != hipSuccess) {
     (void)hipStreamSynchronize(s);  // the staging buffer is reused by the next call
     return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));

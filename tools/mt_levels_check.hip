@@ -25,7 +25,7 @@ int check(uint64_t S, int ki, int back) {
   build_levels(S, ki, back, LV);
   std::vector<const Level*> lv = {&LV[0], &LV[1], &LV[2]};
   std::vector<int> known(S + 1 + kPartRows + 8, 0);
-  known[0] = 1; known[S] = 1;
+  known[0] = 1;  // the caller's array; W_idx (level A's source) is window -1
   int bad = 0;
   for (size_t k = 0; k < lv.size(); ++k) {
     const Level& L = *lv[k];
@@ -38,7 +38,7 @@ int check(uint64_t S, int ki, int back) {
         const JumpJob& j = L.jobs[g + w];
         if (j.src != j0.src || (j.span & 0xffff) != (j0.span & 0xffff)) { bad++; }
         if (j.dst < 0) continue;
-        if (!known[j.src]) { printf("S=%llu lvl %d src %d unknown\n", (unsigned long long)S, k, j.src); return 1; }
+        if (j.src >= 0 && !known[j.src]) { printf("S=%llu lvl %d src %d unknown\n", (unsigned long long)S, k, j.src); return 1; }
         const int lo = j.span & 0xffff, hi = j.span >> 16;
         if (j.poly < ki * kMtJumpRows || j.poly >= (ki + 1) * kMtJumpRows) bad++;
         if (L.comb.empty()) {
