@@ -296,6 +296,56 @@ def _mt_set_state(rng, version, gauss, state, index) -> None:
     rng.setstate((version, tuple(memoryview(state).cast("B").cast("I").tolist()) + (index.value,), gauss))
 
 
+# CPython's random.Random keeps its MT19937 array inside the object —
+# Modules/_randommodule.c: {PyObject_HEAD; int index; uint32_t state[624];},
+# the same in 3.8 .. 3.12 — and a subclass instance keeps those fields at the
+# same offsets.  When this interpreter's layout checks out (once, against
+# getstate() of a probe, reads and a write), the device draws take pointers
+# into the caller's generator and update it in place on success: no
+# getstate / setstate round trip (~36 us of a ~1.5 ms 2^24 make_shares_vec
+# call).  Otherwise (another interpreter, another layout) they marshal.
+_MT_LAYOUT = None  # None: not checked yet; False: unavailable; else (index offset, state offset)
+
+
+def _mt_layout():
+    global _MT_LAYOUT
+    if _MT_LAYOUT is None:
+        _MT_LAYOUT = False
+        try:
+            import _random
+            import random as _rnd
+            import sys
+
+            head = ctypes.sizeof(ctypes.c_ssize_t) + ctypes.sizeof(ctypes.c_void_p)  # ob_refcnt, ob_type
+            off_i, off_s = head, head + 4
+            if sys.implementation.name == "cpython" and _random.Random.__basicsize__ >= off_s + 4 * 624:
+                probe = _rnd.Random(0x5EED)
+                probe.getrandbits(32 * 101)  # index mid-array
+                st = probe.getstate()[1]
+                words = (ctypes.c_uint32 * 624).from_address(id(probe) + off_s)
+                idx = ctypes.c_int32.from_address(id(probe) + off_i)
+                if list(words) == list(st[:624]) and idx.value == st[624]:
+                    words[7] ^= 1
+                    seen = probe.getstate()[1][7]
+                    words[7] ^= 1
+                    if seen == st[7] ^ 1 and probe.getstate() == (3, st, None):
+                        _MT_LAYOUT = (off_i, off_s)
+        except Exception:  # pragma: no cover - any surprise: marshal instead
+            _MT_LAYOUT = False
+    return _MT_LAYOUT
+
+
+def _mt_inplace(rng):
+    """(uint32* state, int32* index) into rng's own MT19937 state, or None."""
+    import _random
+
+    lay = _mt_layout()
+    if not lay or not isinstance(rng, _random.Random):
+        return None
+    return (ctypes.cast(id(rng) + lay[1], ctypes.POINTER(ctypes.c_uint32)),
+            ctypes.cast(id(rng) + lay[0], ctypes.POINTER(ctypes.c_int32)))
+
+
 def mt_skip(rng, words: int) -> None:
     """Advance `rng` (a random.Random) by `words` 32-bit outputs by jump-ahead."""
     version, gauss, state, index = _mt_state(rng)
@@ -319,13 +369,19 @@ def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
     L = lib()
     sb = int(L.dn_mt19937_device_scratch_bytes(n, tm1))
     scratch = torch.empty(sb, dtype=torch.uint8, device=out.device)
-    version, gauss, state, index = _mt_state(rng)
-    rc = L.dn_mt19937_draw_coeffs_device(state, ctypes.byref(index), n, tm1, out.data_ptr(), scratch.data_ptr(), sb,
-                                         stream_ptr())
+    ip = _mt_inplace(rng)  # the entry point writes the state only on success
+    if ip:
+        rc = L.dn_mt19937_draw_coeffs_device(ip[0], ip[1], n, tm1, out.data_ptr(), scratch.data_ptr(), sb,
+                                             stream_ptr())
+    else:
+        version, gauss, state, index = _mt_state(rng)
+        rc = L.dn_mt19937_draw_coeffs_device(state, ctypes.byref(index), n, tm1, out.data_ptr(), scratch.data_ptr(),
+                                             sb, stream_ptr())
     if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
         return False
     check(rc)
-    _mt_set_state(rng, version, gauss, state, index)
+    if not ip:
+        _mt_set_state(rng, version, gauss, state, index)
     return True
 
 
@@ -347,13 +403,19 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
             raise ValueError(f"mt_split_device: {name} must be a contiguous tensor on the shares' HIP device")
     sb = int(L.dn_mt19937_device_scratch_bytes(n, t - 1))
     scratch = torch.empty(sb, dtype=torch.uint8, device=shares.device)
-    version, gauss, state, index = _mt_state(rng)
-    rc = L.dn_mt19937_split_device(state, ctypes.byref(index), secrets.data_ptr(), shares.data_ptr(), n, t, n_shares,
-                                   scratch.data_ptr(), sb, stream_ptr())
+    ip = _mt_inplace(rng)  # the entry point writes the state only on success
+    if ip:
+        rc = L.dn_mt19937_split_device(ip[0], ip[1], secrets.data_ptr(), shares.data_ptr(), n, t, n_shares,
+                                       scratch.data_ptr(), sb, stream_ptr())
+    else:
+        version, gauss, state, index = _mt_state(rng)
+        rc = L.dn_mt19937_split_device(state, ctypes.byref(index), secrets.data_ptr(), shares.data_ptr(), n, t,
+                                       n_shares, scratch.data_ptr(), sb, stream_ptr())
     if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
         return False
     check(rc)
-    _mt_set_state(rng, version, gauss, state, index)
+    if not ip:
+        _mt_set_state(rng, version, gauss, state, index)
     return True
 
 

@@ -319,3 +319,30 @@ def test_mt_jump_job_builder_invariants(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:]
     assert "fails 0" in r.stdout
+
+
+def test_mt_state_in_place_matches_getstate():
+    """The device MT draws update the caller's random.Random in place when
+    this interpreter's layout checks out (_native._mt_layout): the pointers
+    read exactly getstate()'s 624 words and index, a write through them is what
+    getstate() then returns, and a random.Random subclass (the reference's
+    SecretShare.random is one instance of the class) has the same offsets."""
+    assert _native._mt_layout(), "CPython's _random layout: the in-place path is the one this image runs"
+
+    class Sub(random.Random):
+        pass
+
+    for rng in (random.Random(11), Sub(12)):
+        rng.getrandbits(32 * 333)
+        state, index = _native._mt_inplace(rng)
+        words = rng.getstate()[1]
+        assert [state[i] for i in range(624)] == list(words[:624]) and index[0] == words[624]
+        want = random.Random()
+        want.setstate(rng.getstate())
+        state[100] ^= 0xDEADBEEF
+        index[0] = 5
+        st = list(want.getstate()[1])
+        st[100] ^= 0xDEADBEEF
+        st[624] = 5
+        assert list(rng.getstate()[1]) == st
+    assert _native._mt_inplace(object()) is None
