@@ -765,7 +765,8 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
     for (uint32_t done = 0; done < ngroups; ++done) {
       DN_PROBE_SKIP(a, 2u) ring_run<kRun>(R, g, slot, lane);
       wave_sync();
-      DN_PROBE_SKIP(a, 1u) emit_group(a, R + g.o + g.delta + (done & 1u) * group, qb, rbm, 64u * done + lane, nloc, lane);
+      DN_PROBE_SKIP(a, 1u)
+      emit_group(a, R + g.o + g.delta + (done & 1u) * group, qb, rbm, 64u * done + lane, nloc, lane);
       wave_sync();
     }
   } else {
@@ -792,7 +793,8 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
       DN_PROBE_SKIP(a, 2u) ring_run<kRun>(R, g, slot, lane);
       wave_sync();
       nxt = secret_of(gi + 1u);
-      DN_PROBE_SKIP(a, 1u) emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+      DN_PROBE_SKIP(a, 1u)
+      emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
       wave_sync();
     };
     uint64_t secA = secret_of(0), secB = 0;
