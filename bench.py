@@ -611,36 +611,45 @@ def rows_bench(dev, log2n: int) -> dict:
     # device-PRNG split (dn_m521_split_prng, SURVEY §8(d) config 2'): coefficients generated in-kernel
     from delta_node.crypto.shamir import _native as _nat
 
-    sh = torch.empty((5, _field.vec_bytes(n)), dtype=torch.uint8, device=dev)
+    shs = [torch.empty((5, _field.vec_bytes(n)), dtype=torch.uint8, device=dev) for _ in range(3)]
     sec = torch.from_numpy(secrets_int64(3, n)).to(dev)
     prng = {}
+    # The rows before this one end in host-only work (the CPU baselines), and
+    # the GPU clock falls while it idles: the VALU-heavy ChaCha20 split then
+    # reads ~20 % slow for its first tens of milliseconds (scripts/prng_row_probe.py,
+    # profiles/r03/ab/prng_clock/).  So: `warm` (>= 150 ms of the same call),
+    # then per output buffer (three placements, as the draw_split row) the best
+    # of three rounds of `reps` launches; the median over the buffers is quoted.
     for rounds in (20, 8):
-        # The rows before this one end in host-only work (the CPU baselines), and
-        # the GPU clock falls while it idles: the VALU-heavy ChaCha20 split then
-        # reads ~20 % slow for its first tens of milliseconds (scripts/prng_row_probe.py,
-        # profiles/r03/ab/prng_clock/).  So: `warm` (>= 150 ms of the same call),
-        # then the best of three rounds of `reps` launches (each round's mean too).
-        warm(lambda: _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, sh, n, 3, 5))
-        rms = []
-        for _ in range(3):
-            s.record()
-            for _ in range(reps):
-                _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, sh, n, 3, 5)
-            e.record()
-            torch.cuda.synchronize()
-            rms.append(s.elapsed_time(e) / reps)
-        pm = min(rms)
+        by_buf, rounds_ms = [], []
+        warm(lambda: _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, shs[0], n, 3, 5))
+        for sh in shs:
+            rms = []
+            for _ in range(3):
+                s.record()
+                for _ in range(reps):
+                    _nat.split_prng(sec, bytes(range(32)), 0, rounds, 0, sh, n, 3, 5)
+                e.record()
+                torch.cuda.synchronize()
+                rms.append(s.elapsed_time(e) / reps)
+            by_buf.append(min(rms))
+            rounds_ms.append(rms)
+        pm = float(np.median(by_buf))
+        sh = shs[-1]
         back = ss.resolve_shares_vec([sh[1], sh[2], sh[4]], [2, 3, 5], n)
         ops = (2 * 17 / 16) * (12 * 4 * rounds + 32)  # ChaCha lane-ops per element (2.125 blocks)
-        prng[f"chacha{rounds}"] = {"ms": pm, "ms_rounds": rms, "elems_per_s": n / (pm * 1e-3),
+        prng[f"chacha{rounds}"] = {"ms": pm, "ms_by_buffer": by_buf, "ms_rounds": rounds_ms,
+                                   "elems_per_s": n / (pm * 1e-3),
                                    "roofline_hbm": roof("hbm", n * (8 + 5 * 66) / (pm * 1e-3) / 1e9,
                                                         "8 B secret + 5 x 66 B shares per element"),
                                    "roofline_valu": roof("valu", n * ops / (pm * 1e-3) / 1e9,
                                                          f"{ops:.0f} ChaCha lane-ops per element (2.125 blocks)"),
                                    "roundtrip_equal": bool(torch.equal(back, sec))}
     rows["split_prng"] = {"workload": f"3-of-5 split of 2^{log2n} int64, coefficients generated on the device "
-                                      f"(338 B/elem HBM)", **prng}
-    del sh, sec, back
+                                      f"(338 B/elem HBM)",
+                          "timing": "median over three output buffers of the best of three rounds of "
+                                    f"{reps} launches each, after >= 0.15 s of warm-up launches", **prng}
+    del shs, sh, sec, back
     # coordinator member sum: 10 int64 members
     from delta_node.utils import sum_int64
 
@@ -746,31 +755,40 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
 
     n = 1 << log2n
     sec = torch.from_numpy(secrets_int64(5, n)).to(dev)
-    out = torch.empty((5, field.vec_bytes(n)), dtype=torch.uint8, device=dev)
-    fused, unfused = [], []
+    # the fused call's generation writes the shares at the rate of their pages'
+    # placement: three separately allocated outputs, the
+    # best of `reps` calls on each, the median of the three quoted
+    outs = [torch.empty((5, field.vec_bytes(n)), dtype=torch.uint8, device=dev) for _ in range(3)]
+    fused_by_buf, unfused = [], []
     ok = True
     wss = shamir.SecretShare(3)
-    warm(lambda: wss.make_shares_vec(sec, 5, out=out))
-    for r in range(reps + 1):
-        a, b = shamir.SecretShare(3), shamir.SecretShare(3)
-        a.random.seed(77 + r)
-        b.random.seed(77 + r)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        got = a.make_shares_vec(sec, 5, out=out)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        co = b.draw_coeffs_vec(n, dev)
-        want = torch.empty_like(out)
-        _native.split_u64(sec, co, want, n, 3, 5)
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        if r:  # the first round warms up
-            fused.append(t1 - t0)
-            unfused.append(t2 - t1)
-        ok = ok and bool(torch.equal(got, want)) and a.random.getstate() == b.random.getstate()
-        del co, want
-    fm, um = min(fused), min(unfused)
+    warm(lambda: wss.make_shares_vec(sec, 5, out=outs[0]))
+    for bi, out in enumerate(outs):
+        fused = []
+        for r in range(reps + 1):
+            a, b = shamir.SecretShare(3), shamir.SecretShare(3)
+            a.random.seed(77 + r)
+            b.random.seed(77 + r)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            got = a.make_shares_vec(sec, 5, out=out)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if r:  # the first call on each buffer warms up
+                fused.append(t1 - t0)
+            if bi == 0:  # draw then split, and the parity check, once
+                co = b.draw_coeffs_vec(n, dev)
+                want = torch.empty_like(out)
+                _native.split_u64(sec, co, want, n, 3, 5)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                if r:
+                    unfused.append(t2 - t1)
+                ok = ok and bool(torch.equal(got, want)) and a.random.getstate() == b.random.getstate()
+                del co, want
+        fused_by_buf.append(min(fused))
+    fm, um = float(np.median(fused_by_buf)), min(unfused)
+    del outs
     words = 17 * 2 * n
     # smaller vectors take shorter MT substreams (2^10 / 2^12 / 2^14 draws: dn_mt19937_split_device)
     by_size = {}
@@ -797,6 +815,9 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
             "draw_then_split_elems_per_s": n / um, "mt_words_per_s_fused": words / fm,
             "roofline_fused": roof("hbm", n * (8 + 5 * 66) / fm / 1e9,
                                    "8 B secret + 5 x 66 B shares per element (wall time of the whole call)"),
+            "fused_ms_by_buffer": [x * 1e3 for x in fused_by_buf],
+            "timing": "wall time per call; fused_ms: the median over three output buffers of the best of "
+                      f"{reps} calls on each (after >= 0.15 s of warm-up calls)",
             "equal_draw_then_split_and_state": ok, "fused_ms_by_size": by_size}
 
 
