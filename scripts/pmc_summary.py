@@ -7,7 +7,7 @@ coalesced streaming read (TCC_EA0_RDREQ x 64 B for 128-B requests), so read
 bytes = 2 x FETCH_SIZE x 1024 (cross-checked with TCC_EA0_RDREQ x 128 B);
 WRITE_SIZE x 1024 is exact for streaming stores.
 
-usage: pmc_summary.py <dir with pmc_fetch.csv pmc_write.csv pmc_req.csv> <out.json> [log2n]
+usage: pmc_summary.py <dir with pmc_fetch.csv pmc_write.csv pmc_req.csv> <out.json> [log2n] [source note]
 """
 import csv
 import json
@@ -24,7 +24,7 @@ for name in ("pmc_fetch", "pmc_write", "pmc_req"):
             kn = row["Kernel_Name"]
             k = ("split" if "split_kernel" in kn else
                  "reconstruct" if "reconstruct_kernel" in kn else
-                 "fused_draw_split" if "mt_gen_kernel<3>" in kn else
+                 "fused_draw_split" if "mt_gen_kernel<3" in kn else
                  "mask_accumulate" if "bounded_acc_kernel" in kn else None)
             if k:
                 vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
@@ -32,7 +32,7 @@ alg = {"split": N * (8 + 2 * 66 + 5 * 66), "reconstruct": N * (3 * 66 + 8),
        "fused_draw_split": N * (8 + 5 * 66), "mask_accumulate": N * 16}
 alg_rw = {"split": (N * (8 + 2 * 66), N * 5 * 66), "reconstruct": (N * 3 * 66, N * 8),
           "fused_draw_split": (N * 8, N * 5 * 66), "mask_accumulate": (N * 8, N * 8)}
-res = {"N": N, "workload": "3-of-5 split / reconstruct xs=1,3,5 -> int64, 2^24 elements; fused MT draw + split "
+res = {"source": sys.argv[4] if len(sys.argv) > 4 else f"rocprofv3 --pmc passes summarised from {d}", "N": N, "workload": "3-of-5 split / reconstruct xs=1,3,5 -> int64, 2^24 elements; fused MT draw + split "
                      "(make_shares_vec); mask accumulate (10 generators, float64 base)", "kernels": {}}
 for k, c in vals.items():
     if not c.get("FETCH_SIZE") or not c.get("WRITE_SIZE") or not c.get("TCC_EA0_RDREQ_sum"):
