@@ -114,6 +114,7 @@ struct JumpArgs {
   uint32_t* wins;  // window s at row s (row 0 the caller's array), the caller's window advanced idx words at row -1
   const JumpJob* jobs;
   uint32_t njobs;
+  uint32_t probe;  // tuning build only (DN_MT_JUMP_PROBE): 1 = no Horner steps, 2 = no stream stepping (timing only)
 };
 
 // Jump and generation waves keep a 624-word MT window in registers: Q[11] a
@@ -256,7 +257,7 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
     uint32_t* ring = E;
     for (uint32_t i = tid; i < kMtN; i += 64u * W) ring[i] = src[i];
     __syncthreads();
-    const uint32_t need = 64u * static_cast<uint32_t>(lo) + 687u;
+    const uint32_t need = a.probe == 2u ? 687u : 64u * static_cast<uint32_t>(lo) + 687u;
     for (uint32_t base = 0; base + kMtN < need; base += kMtN - kMtM) {
       if (tid < static_cast<uint32_t>(kMtN - kMtM)) {
         const uint32_t i = base + tid;
@@ -303,8 +304,9 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   while (top > lo && g[top] == 0ull) --top;  // steps above it leave r = 0
   // runs of 11 steps (the frame returns to Q[0] after 11) ending at word lo;
   // r = 0 before the first nonzero word, so a run starts with zero words above it
-  for (int wi = lo + 11 * ((top - lo) / 11) + 10; wi >= lo + 10; wi -= 11)
-    jump_run(Q, L, E, off, g, wi, top, std::make_integer_sequence<int, 11>{});
+  if (a.probe != 1u)
+    for (int wi = lo + 11 * ((top - lo) / 11) + 10; wi >= lo + 10; wi -= 11)
+      jump_run(Q, L, E, off, g, wi, top, std::make_integer_sequence<int, 11>{});
   uint32_t* dst = a.wins + static_cast<uint64_t>(dsti) * kMtN;
 #pragma unroll
   for (int r = 0; r < 11; ++r) {
@@ -1122,7 +1124,9 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   for (int k = 0; k < 3; ++k) {
     const Level& l = lv[k];
     if (!l.jobs.empty()) {
-      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.jobs.size())};
+      const char* jpr = tune_env("DN_MT_JUMP_PROBE");
+      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.jobs.size()),
+                        jpr ? static_cast<uint32_t>(std::atoi(jpr)) : 0u};
       const dim3 grid(static_cast<uint32_t>(l.jobs.size() / static_cast<size_t>(l.W)));
       if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, s, ja);
       else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, s, ja);
