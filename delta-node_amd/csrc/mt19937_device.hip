@@ -95,6 +95,10 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // ------------------------------------------------------------------ jumps
+#ifndef DN_JUMP_TABLE_POS
+#define DN_JUMP_TABLE_POS 1  // jump table built per stream position (1) or per table word (0; A/B builds)
+#endif
+
 struct JumpJob {
   int32_t src, poly, dst;  // window indices (dst < 0: padding), jump-table row
   int32_t span;            // words [lo, hi) of g this job evaluates: lo | hi << 16
@@ -268,6 +272,34 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
     for (uint32_t i = tid; i < 687u; i += 64u * W) ext[i] = ring[(64u * static_cast<uint32_t>(lo) + i) & 1023u];
     __syncthreads();
   }
+#if DN_JUMP_TABLE_POS
+  // One thread per stream position q = 64 k + m (row k = 0..10 of the frame,
+  // m = 0..63; T-stream word j = q - 16, zero outside 0..683): the 16
+  // combinations of words j..j+3 from four LDS reads, stored to the main half
+  // (row k = 2 i + parity, k <= 9) and the wrap half (k = 2 i + parity + 1,
+  // k >= 1) of pair plane i.  The gap before the wrap half and the planes'
+  // pad words are never read.
+  for (uint32_t q = tid; q < 704u; q += 64u * W) {
+    const int j = static_cast<int>(q) - 16;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (j >= 0 && j < 684) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) w[b] = ext[j + b];
+    }
+    const uint32_t k = q >> 6, m = q & 63u;
+    uint32_t* em = k <= 9u ? E + (k >> 1) * kEPair + 2u * m + (k & 1u) : nullptr;
+    uint32_t* ew = k >= 1u ? E + kEWrap + ((k - 1u) >> 1) * kEPair + 2u * m + ((k - 1u) & 1u) : nullptr;
+    uint32_t c[16];
+    c[0] = 0u;
+#pragma unroll
+    for (int v = 1; v < 16; ++v) c[v] = c[v & (v - 1)] ^ w[__builtin_ctz(v)];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      if (em) em[v * kEVWords] = c[v];
+      if (ew) ew[v * kEVWords] = c[v];
+    }
+  }
+#else
   for (uint32_t e = tid; e < static_cast<uint32_t>(kEWords); e += 64u * W) {
     const uint32_t wrap = e >= static_cast<uint32_t>(kEWrap) ? 1u : 0u, re = e - wrap * kEWrap;
     const uint32_t i = re / kEPair, rem = re - i * kEPair;  // pair plane, position in it
@@ -281,6 +313,7 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
     }
     E[e] = x;
   }
+#endif
   __syncthreads();
   if (j0 + wid >= a.njobs || dsti < 0) return;
 
