@@ -893,6 +893,32 @@ void push_groups(Level& L, int32_t src, const std::vector<std::pair<int32_t, int
 // 16) part jobs of one source and part per workgroup (one table): ~256
 // workgroups, one per CU (82 KB of LDS each), 2..16 waves.  Large levels
 // (n >= 4096) stay whole, 16 jumps per workgroup.
+// Word ranges [cut[j], cut[j + 1]) of g for at most P parts.  A part costs
+// its Horner steps — whole runs of 11 words (jump_run), the words above g's
+// top included — plus the stepping of its source stream to word 64 lo, about
+// r runs' worth per word of lo (r ~ 0.053 / 11 for 8-wave workgroups, ~0.014 / 11
+// for 16-wave ones: profiles/r03/ab/jump_probe/).  Parts nearer the top of g
+// start further down the stream, so they get fewer runs: the smallest cost
+// bound T (in steps) the greedy split meets with at most P parts.
+std::vector<int32_t> part_cuts(int P, int W) {
+  const double r = W >= 16 ? 0.014 : 0.053;  // stepping cost per word of lo, in Horner steps
+  const int runs_total = (kMtPolyWords + 10) / 11;
+  for (int T = 11; ; T += 1) {
+    std::vector<int32_t> cut{0};
+    while (cut.back() < kMtPolyWords && static_cast<int>(cut.size()) <= P) {
+      const int lo = cut.back();
+      const int runs = static_cast<int>((T - r * lo) / 11.0);
+      if (runs < 1) break;
+      cut.push_back(std::min(kMtPolyWords, lo + 11 * runs));
+    }
+    if (cut.back() >= kMtPolyWords && static_cast<int>(cut.size()) - 1 <= P) return cut;
+    if (T > 11 * runs_total + 1000) break;
+  }
+  std::vector<int32_t> cut;  // unreachable: one part of all the words
+  for (int j = 0; j <= P; ++j) cut.push_back(kMtPolyWords * j / P);
+  return cut;
+}
+
 void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs,
                 int32_t prow0) {
   size_t n = 0, most = 0;  // jumps, and the most of one source
@@ -908,6 +934,8 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
     for (auto& sp : srcs) push_groups(L, sp.first, sp.second, per);
     return;
   }
+  const std::vector<int32_t> cut = part_cuts(P, L.W);
+  P = static_cast<int>(cut.size()) - 1;
   int32_t row = prow0;
   for (auto& sp : srcs)
     for (auto& pd : sp.second) {
@@ -915,7 +943,7 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
       row += P;
     }
   for (int j = 0; j < P; ++j) {
-    const int32_t lo = kMtPolyWords * j / P, hi = kMtPolyWords * (j + 1) / P;
+    const int32_t lo = cut[j], hi = cut[j + 1];
     row = prow0 + j;
     for (auto& sp : srcs) {
       std::vector<std::pair<int32_t, int32_t>> pd;
