@@ -883,14 +883,17 @@ def launcher_cmd(gpus: int, argv, port: int) -> list:
 
 
 def launch_ranks(gpus: int, argv) -> int:
-    """Run N ranks through torch.distributed.run as a child (never exec: this
-    process has made no GPU call and makes none), pass its output through,
-    and print rank 0's JSON line as the one line on stdout.  Returns the
-    child's exit code."""
+    """Run N ranks through torch.distributed.run as a child process (never
+    exec), pass its output through, and print rank 0's JSON line as the one
+    line on stdout.  Returns the child's exit code.  The parent launches no
+    kernel and allocates nothing on a GPU; counting devices may initialise
+    the HIP runtime in it (torch.cuda.device_count falls back to
+    hipGetDeviceCount without amdsmi), which is harmless because the ranks
+    are a separate child process, not an exec of this one."""
     import subprocess
 
     backend = os.environ.get("DN_DIST_BACKEND", "nccl")
-    visible = torch.cuda.device_count()  # counts devices without initialising HIP
+    visible = torch.cuda.device_count()  # may initialise HIP here (see above)
     if backend == "nccl" and gpus > visible:
         print(f"bench.py: --gpus {gpus} with RCCL needs {gpus} visible GPUs, this node has {visible} "
               "(DN_DIST_BACKEND=gloo rehearses the ranks on fewer GPUs)", file=sys.stderr)
@@ -1185,8 +1188,18 @@ def main():
         line["rows"]["byte_api"] = byte_api_row()
     if args.config5 and world == 1:
         line["config5"] = config5_bench(args.log2n)
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
-        line["cpu_baseline"] = cpu_baseline(t, n, xs, args.cpu_budget)
+    if args.cpu_budget > 0:
+        # the reference CPU path timed on this host in the same run, at every
+        # N (north_star): after all GPU work, rank 0 only, while the other
+        # ranks wait at a barrier (their GPU work is done; their cores idle)
+        if dist_on:
+            barrier()
+        if rank == 0:
+            procs = min(16, max(1, (os.cpu_count() or 16) // world))
+            line["cpu_baseline"] = cpu_baseline(t, n, xs, args.cpu_budget, procs=procs)
+            line["cpu_baseline"]["run_at_world_size"] = world
+        if dist_on:
+            barrier()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist_on:

@@ -498,6 +498,39 @@ extern "C" int dn_shamir_make_shares_host(const uint8_t* value, uint64_t value_l
   return DN_OK;
 }
 
+// _eval_at (shamir.py:19-25) for any integers: Horner from the top with
+// `value %= prime` after each step, Python's signed % (the result takes the
+// sign of the modulus).  Signed values travel as magnitude BE + sign flag.
+extern "C" int dn_shamir_eval_at_host(const uint8_t* coeffs_be, const uint64_t* coeff_offsets,
+                                      const uint8_t* coeff_neg, int n_coeffs, const uint8_t* x_be, uint32_t x_len,
+                                      int x_neg, const uint8_t* prime_be, uint32_t prime_len, int prime_neg,
+                                      uint8_t* out, uint64_t out_cap, uint64_t* out_len, int* out_neg) {
+  if (n_coeffs < 0 || !out_len || !out_neg || (n_coeffs && (!coeffs_be || !coeff_offsets)) ||
+      (x_len && !x_be) || (prime_len && !prime_be))
+    return set_error(DN_ERR_ARG, "dn_shamir_eval_at_host: bad arguments");
+  *out_len = 0;
+  *out_neg = 0;
+  if (n_coeffs == 0) return DN_OK;  // the loop never runs: value = 0
+  BN p = bn_from_be(prime_be, prime_len);
+  if (p.zero()) return set_error(DN_ERR_ZERODIV, "integer division or modulo by zero");
+  BN x = bn_from_be(x_be, x_len);
+  x.neg = x_neg && !x.zero();
+  BN v{};
+  for (int j = n_coeffs - 1; j >= 0; --j) {
+    BN c = bn_from_be(coeffs_be + coeff_offsets[j], coeff_offsets[j + 1] - coeff_offsets[j]);
+    c.neg = coeff_neg && coeff_neg[j] && !c.zero();
+    v = bn_mod(bn_add(bn_mul(v, x), c), p);  // in [0, |p|)
+    if (prime_neg && !v.zero()) {            // Python: (a % -m) == (a % m) - m when nonzero
+      v = sub_mag(p, v);
+      v.neg = true;
+    }
+  }
+  if (out_cap < v.m.size() * 4) return set_error(DN_ERR_ARG, "dn_shamir_eval_at_host: output capacity too small");
+  *out_len = bn_to_be_min(v, out);
+  *out_neg = v.neg ? 1 : 0;
+  return DN_OK;
+}
+
 extern "C" int dn_shamir_resolve_shares_host(const uint8_t* shares, const uint64_t* offsets, int k, int threshold,
                                              const uint8_t* prime_be, uint32_t prime_len, uint8_t* out,
                                              uint64_t out_cap, uint64_t* out_len) {

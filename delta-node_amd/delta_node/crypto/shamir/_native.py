@@ -46,6 +46,7 @@ EXPORTS = (
     "dn_m521_split_prng", "dn_m521_prng_coeffs",
     "dn_mt19937_device_scratch_bytes", "dn_mt19937_draw_coeffs_device", "dn_mt19937_skip",
     "dn_mt19937_split_device", "dn_mt19937_split_supported", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
+    "dn_shamir_eval_at_host", "dn_block_granularity", "dn_block_alloc", "dn_block_free",
 )
 
 
@@ -150,6 +151,16 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_shamir_resolve_shares_host.restype = i32
     L.dn_shamir_resolve_shares_host.argtypes = [ctypes.c_char_p, vp, i32, i32, ctypes.c_char_p, ctypes.c_uint32, vp,
                                                 u64, ctypes.POINTER(ctypes.c_uint64)]
+    L.dn_shamir_eval_at_host.restype = i32
+    L.dn_shamir_eval_at_host.argtypes = [ctypes.c_char_p, vp, ctypes.c_char_p, i32, ctypes.c_char_p,
+                                         ctypes.c_uint32, i32, ctypes.c_char_p, ctypes.c_uint32, i32, vp, u64,
+                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
+    L.dn_block_granularity.restype = i32
+    L.dn_block_granularity.argtypes = [i32, ctypes.POINTER(ctypes.c_uint64)]
+    L.dn_block_alloc.restype = i32
+    L.dn_block_alloc.argtypes = [u64, u64, i32, ctypes.POINTER(ctypes.c_void_p)]
+    L.dn_block_free.restype = i32
+    L.dn_block_free.argtypes = [vp]
     L.dn_mt19937_skip.restype = i32
     L.dn_mt19937_skip.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), u64]
     L.dn_last_error.restype = ctypes.c_char_p
@@ -175,7 +186,7 @@ def check(rc: int) -> None:
     if rc == DN_ERR_UNSUPPORTED:
         raise NotImplementedError(msg)
     if rc == DN_ERR_ZERODIV:
-        raise ZeroDivisionError
+        raise ZeroDivisionError(*([] if msg == "ZeroDivisionError" else [msg]))
     if rc == DN_ERR_ASSERT:
         raise AssertionError
     if rc == DN_ERR_OVERFLOW:
@@ -335,12 +346,30 @@ def _mt_layout():
     return _MT_LAYOUT
 
 
+# The methods through which the reference's `self.random.randint(1, p - 1)`
+# (shamir.py:60) reaches the MT19937 words.  A subclass overriding any of them
+# (random.SystemRandom: os.urandom; a recording or seeded-differently
+# generator) draws something else, so the MT paths below must not serve it.
+_MT_METHODS = ("randint", "randrange", "_randbelow", "getrandbits", "random", "getstate", "setstate", "seed")
+
+
+def mt_compatible(rng) -> bool:
+    """True when `rng.randint` is CPython's MT19937 draw: a random.Random
+    whose class overrides none of the methods the draw goes through.  Only
+    then may the device / host MT paths (jump-ahead, the caller's state read
+    directly) replace the reference's per-coefficient calls."""
+    import random as _rnd
+
+    if not isinstance(rng, _rnd.Random):
+        return False
+    cls = type(rng)
+    return all(getattr(cls, m, None) is getattr(_rnd.Random, m) for m in _MT_METHODS)
+
+
 def _mt_inplace(rng):
     """(uint32* state, int32* index) into rng's own MT19937 state, or None."""
-    import _random
-
     lay = _mt_layout()
-    if not lay or not isinstance(rng, _random.Random):
+    if not lay or not mt_compatible(rng):
         return None
     return (ctypes.cast(id(rng) + lay[1], ctypes.POINTER(ctypes.c_uint32)),
             ctypes.cast(id(rng) + lay[0], ctypes.POINTER(ctypes.c_int32)))
@@ -467,6 +496,35 @@ def host_resolve_shares(shares: Sequence[bytes], threshold: int, prime: int) -> 
     if rc:
         check(rc)
     return ctypes.string_at(out, n.value)
+
+
+def _mag(v: int) -> bytes:
+    v = abs(v)
+    return v.to_bytes((v.bit_length() + 7) // 8, "big")
+
+
+def host_eval_at(coeffs: Sequence[int], x: int, prime: int) -> int:
+    """`_eval_at` (shamir.py:19-25) for any integers on the host
+    (dn_shamir_eval_at_host): Horner with Python's `% prime` after each step."""
+    k = len(coeffs)
+    mags = [_mag(c) for c in coeffs]
+    offs = (ctypes.c_uint64 * (k + 1))()
+    o = 0
+    for i, m in enumerate(mags):
+        offs[i] = o
+        o += len(m)
+    offs[k] = o
+    neg = bytes(int(c < 0) for c in coeffs)
+    xb, pb = _mag(x), _mag(prime)
+    cap = max(len(pb), 1) + 8
+    out = ctypes.create_string_buffer(cap)
+    n, sgn = ctypes.c_uint64(0), ctypes.c_int(0)
+    rc = (_lib or lib()).dn_shamir_eval_at_host(b"".join(mags), offs, neg, k, xb, len(xb), int(x < 0), pb, len(pb),
+                                                int(prime < 0), out, cap, ctypes.byref(n), ctypes.byref(sgn))
+    if rc:
+        check(rc)
+    v = int.from_bytes(ctypes.string_at(out, n.value), "big")
+    return -v if sgn.value else v
 
 
 def version() -> str:

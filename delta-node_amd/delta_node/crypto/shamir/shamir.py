@@ -91,16 +91,32 @@ def _eval_many(coeffs: Sequence[int], n_shares: int) -> List[int]:
 
 
 def _eval_at(coeffs: List[int], x: int, prime: int) -> int:
-    """Horner evaluation of `coeffs` at x mod prime (shamir.py:19-25), on the GPU."""
-    if prime != PRIME:
-        raise NotImplementedError("the MI355X Shamir path supports only the default prime 2^521 - 1")
+    """Horner evaluation of `coeffs` at x mod prime (shamir.py:19-25).
+
+    GF(2^521 - 1) with 1 <= x <= 65535 and at most 64 coefficients runs the
+    device split (`dn_m521_split_fe`); every other input — another prime
+    (negative too), x = 0, a negative or larger x, more coefficients — runs
+    the library's host Horner (`dn_shamir_eval_at_host`), which computes
+    exactly what the reference's loop computes for any integers."""
     if not coeffs:
         return 0
-    if x == 0:
-        return coeffs[0] % prime
-    if not 1 <= x <= _native.MAX_SHARES or len(coeffs) > _native.MAX_THRESHOLD:
-        raise NotImplementedError("_eval_at: x must be in 1..65535 and len(coeffs) <= 64")
-    return _eval_many([c % prime for c in coeffs], x)[x - 1]
+    if prime == PRIME and 1 <= x <= _native.MAX_SHARES and len(coeffs) <= _native.MAX_THRESHOLD:
+        return _eval_many([c % prime for c in coeffs], x)[x - 1]
+    return _native.host_eval_at([int(c) for c in coeffs], int(x), int(prime))
+
+
+def _draw_coeffs_generic(rng, n: int, tm1: int):
+    """The reference's own draw for a generator that is not plain MT19937
+    (random.SystemRandom, a subclass overriding randint / getrandbits ...):
+    `rng.randint(1, p - 1)` per coefficient, element-major (shamir.py:59-61),
+    packed as a host block [tm1, vec_bytes(n)]."""
+    import numpy as np
+
+    cols = [[0] * n for _ in range(tm1)]
+    for e in range(n):
+        for j in range(tm1):
+            cols[j][e] = rng.randint(1, PRIME - 1)
+    return np.stack([field.ints_to_vec(c) for c in cols])
 
 
 def _lagrange_generic(xs: Sequence[int], prime: int) -> List[int]:
@@ -207,6 +223,15 @@ class SecretShare(object):
         dev = device if device is not None else _device()
         tm1 = max(self.threshold, 1) - 1
         sharded = elem_offset != 0 or (n_total is not None and n_total != n)
+        if not _native.mt_compatible(self.random):
+            # not CPython's MT19937 draw: call it, as the reference does
+            if sharded:
+                raise NotImplementedError("draw_coeffs_vec: a sharded draw needs a plain random.Random "
+                                          f"(jump-ahead), not {type(self.random).__name__}")
+            self.last_draw_rejected = False
+            if tm1 <= 0 or n <= 0:
+                return torch.zeros((max(tm1, 0), field.vec_bytes(n)), dtype=torch.uint8, device=dev)
+            return torch.from_numpy(_draw_coeffs_generic(self.random, n, tm1)).to(dev)
         if sharded:
             if n_total is None or not 0 <= elem_offset <= elem_offset + n <= n_total:
                 raise ValueError("draw_coeffs_vec: shard [elem_offset, elem_offset + n) must lie in [0, n_total)")
@@ -267,8 +292,8 @@ class SecretShare(object):
         elif (out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous()
               or out.device != dev):
             raise ValueError(f"make_shares_vec: out must be contiguous uint8 [{shares}, {vb}] on {dev}")
-        if coeffs is None and t > 1 and n > 0 and shares > 0 and _native.mt_split_device(self.random, vals, out, n, t,
-                                                                                          shares):
+        if (coeffs is None and t > 1 and n > 0 and shares > 0 and _native.mt_compatible(self.random)
+                and _native.mt_split_device(self.random, vals, out, n, t, shares)):
             # fused: the reference's MT19937 draws feed the split in registers (no coefficient block)
             self.last_draw_rejected = False
             return out

@@ -245,6 +245,37 @@ int dn_shamir_resolve_shares_host(const uint8_t* shares, const uint64_t* offsets
                                   uint64_t* out_len);
 
 /*
+ * Host.  `_eval_at(coeffs, x, prime)` (shamir.py:19-25) for any integers, the
+ * general case the device split does not take (another prime, x outside
+ * 1..65535, more than 64 coefficients, negative operands): Horner from the
+ * top with Python's `value %= prime` after every step.  Coefficient j is
+ * bytes coeff_offsets[j] .. coeff_offsets[j+1] of coeffs_be (magnitude, big
+ * endian) with sign coeff_neg[j] (NULL: all non-negative); x and prime are
+ * magnitude + sign likewise.  The result (sign of the modulus, as Python) is
+ * written minimal big-endian to out, its sign to *out_neg.  n_coeffs == 0
+ * gives 0 (the reference's loop never runs); prime == 0 with coefficients is
+ * DN_ERR_ZERODIV, as Python's `%`.
+ */
+int dn_shamir_eval_at_host(const uint8_t* coeffs_be, const uint64_t* coeff_offsets, const uint8_t* coeff_neg,
+                           int n_coeffs, const uint8_t* x_be, uint32_t x_len, int x_neg, const uint8_t* prime_be,
+                           uint32_t prime_len, int prime_neg, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
+                           int* out_neg);
+
+/*
+ * Host.  Opt-in share-block allocator (csrc/vmm_block.cpp): `bytes` of device
+ * memory on `device` built from physical chunks of chunk_bytes (rounded up to
+ * the allocation granularity; 0 = 2 MiB) mapped back to back into one
+ * reserved virtual range.  The split's rate depends on the physical pages of
+ * its share block; this lets a caller choose the block's
+ * composition.  dn_block_free synchronises the device, then unmaps and
+ * releases every chunk.  Every other entry point keeps taking caller-owned
+ * memory from any allocator.
+ */
+int dn_block_granularity(int device, uint64_t* bytes);
+int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, void** ptr);
+int dn_block_free(void* ptr);
+
+/*
  * Host.  Advance a CPython MT19937 state by `words` 32-bit outputs (as
  * `words` getrandbits(32) calls would) by jump-ahead instead of stepping.
  */

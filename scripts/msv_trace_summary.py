@@ -2,7 +2,7 @@
 """One make_shares_vec call's GPU timeline from a rocprofv3 kernel trace (+
 memory-copy trace): the ops of the last call (the stretch after the last
 jump-level launch's preceding gap > 200 us), with start offsets, durations
-and the gaps between them.  usage: msv_trace_summary.py <dir with csvs>"""
+and the gaps between them.  usage: msv_trace_summary.py <dir with csvs> [calls to keep, default 3]"""
 import csv
 import glob
 import json
@@ -26,7 +26,8 @@ for o in ops:
     cur.append(o)
 calls.append(cur)
 out = []
-for c in calls[-3:]:
+keep = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+for c in calls[-keep:]:
     t0 = c[0][0]
     rows, prev = [], None
     for s, e, n in c:

@@ -21,6 +21,6 @@ for i in 1 2; do
   echo "== prng new $i" && timeout -k 10 120 python scripts/prng_ab.py >> $O/prng_ab.jsonl 2>> $O/ab.err || { rc=$?; break; }
 done
 cut -c1-330 $O/prng_ab.jsonl
-if [ $rc = 0 ]; then TAG=${TAG:-r03e}_full STAGES=tests,smoke,bench,prof bash scripts/gpu_r03.sh || rc=$?; fi
+if [ $rc = 0 ]; then TAG=${TAG:-r03e}_full STAGES=tests,smoke,bench,prof bash scripts/passes/gpu_r03.sh || rc=$?; fi
 echo "== rc $rc"
 exit $rc

@@ -11,6 +11,6 @@ export TMPDIR=/tmp
 rc=0
 echo "== mt aux" && AUXES=2,0,16,1,18 timeout -k 10 240 python scripts/mt_aux_probe.py > $O/mt_aux.json 2> $O/mt_aux.err || rc=$?
 cut -c1-400 $O/mt_aux.json
-if [ $rc = 0 ]; then TAG=${TAG:-r03f}_pmc KINDS="aes msv prng" bash scripts/gpu_pmc_r03.sh || rc=$?; fi
+if [ $rc = 0 ]; then TAG=${TAG:-r03f}_pmc KINDS="aes msv prng" bash scripts/passes/gpu_pmc_r03.sh || rc=$?; fi
 echo "== rc $rc"
 exit $rc

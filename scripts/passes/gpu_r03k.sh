@@ -3,7 +3,7 @@
 # permutes (product) against DN_JUMP_PIPE=0 (scripts/ab_msv.sh, BASE=nopipe);
 # (2) the PRNG split with two / four tiles' top-limb blocks per pass (product)
 # against one (lib/ab/libdn_shamir_notp.so), alternating, after the PRNG tests;
-# (3) the PRNG grid-cap sweep (scripts/gpu_r03j.sh).
+# (3) the PRNG grid-cap sweep (scripts/passes/gpu_r03j.sh).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
@@ -24,6 +24,6 @@ for rep in 1 2 3; do
   done
 done
 cat $O/prng_tp.jsonl
-if [ $rc = 0 ]; then TAG=${TAG:-r03k}/cap CAPS="0 512 1024 2048 4096" bash scripts/gpu_r03j.sh || rc=$?; fi
+if [ $rc = 0 ]; then TAG=${TAG:-r03k}/cap CAPS="0 512 1024 2048 4096" bash scripts/passes/gpu_r03j.sh || rc=$?; fi
 echo "== rc $rc"
 exit $rc

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 pass v: the one-copy MT scratch layout — MT / fused / sharded GPU
 # tests and the small-bench rows test, one make_shares_vec call's GPU
-# timeline, then the level-B part-count sweep (scripts/gpu_r03u.sh).
+# timeline, then the level-B part-count sweep (scripts/passes/gpu_r03u.sh).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
@@ -17,6 +17,6 @@ if [ $rc = 0 ]; then
   python3 scripts/msv_trace_summary.py /tmp/prof_msv > $O/msv_timeline.json 2>> $O/msv_trace.err || true
   cat $O/msv_wall.json
 fi
-if [ $rc = 0 ]; then TAG=${TAG:-r03v}/parts bash scripts/gpu_r03u.sh || rc=$?; fi
+if [ $rc = 0 ]; then TAG=${TAG:-r03v}/parts bash scripts/passes/gpu_r03u.sh || rc=$?; fi
 echo "== rc $rc"
 exit $rc

@@ -9,7 +9,7 @@ O=gpurun_out/${TAG:-r03y}
 mkdir -p $O
 export TMPDIR=/tmp
 rc=0
-TAG=${TAG:-r03y} STAGES=tests,smoke,bench,prof bash scripts/gpu_r03.sh || rc=$?
+TAG=${TAG:-r03y} STAGES=tests,smoke,bench,prof bash scripts/passes/gpu_r03.sh || rc=$?
 if [ $rc = 0 ]; then
   echo "== 4-rank gloo rehearsal" && DN_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 --steps 5 --warmup 2 \
       --rows 0 --config5 0 --cpu-budget 0 --config4 1 --config4-log2n 22 > $O/bench4_gloo.json 2> $O/bench4_gloo.err || rc=$?

@@ -3,6 +3,9 @@
 
     python tests/golden/make_golden.py            # small fixtures + 2^16/2^20 digests
     python tests/golden/make_golden.py --big      # adds the 2^24 split digest (~5 min)
+    python tests/golden/make_golden.py --only recon_135_2e24,recon_245_2e24,split_t5n9_2e22
+                                                  # just the named full-size digests, one
+                                                  # process each, merged into manifest.json
 
 The reference `delta_node/crypto/shamir/shamir.py` is loaded by file path
 (`_ref_loader.py`); every expected value below is an output of the reference's
@@ -215,12 +218,44 @@ def recon_digest(xs, N, mt_seed):
             "input_digest": combine_digests(chunks_in), "digest": combine_digests(chunks_out)}
 
 
+# Full-size pins of BASELINE configs 2-4 (one reference process each, minutes).
+BIG_DIGESTS = {
+    "split_t3n5_2e24": lambda: split_digest(3, 5, 1 << 24, 1, 1),
+    # config 3: reconstruct of 2^24 elements from random (inconsistent) share
+    # values, the same element-major MT stream as the 2^18 digests
+    "recon_135_2e24": lambda: recon_digest([1, 3, 5], 1 << 24, 31),
+    "recon_245_2e24": lambda: recon_digest([2, 4, 5], 1 << 24, 32),
+    # config 4's 5-of-9 split at 2^22 (2^26 would take the reference ~1.5 h)
+    "split_t5n9_2e22": lambda: split_digest(5, 9, 1 << 22, 13, 3),
+}
+
+
+def _run_big(name):
+    t0 = time.time()
+    d = BIG_DIGESTS[name]()
+    d["name"] = name
+    print(f"{name} done {time.time() - t0:.1f}s", flush=True)
+    return d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true", help="also the 2^24 split digest")
+    ap.add_argument("--only", default="", help="comma-separated BIG_DIGESTS names; nothing else")
     args = ap.parse_args()
     path = os.path.join(HERE, "manifest.json")
     man = json.load(open(path)) if os.path.exists(path) else {}
+    if args.only:
+        import multiprocessing as mp
+        names = args.only.split(",")
+        with mp.get_context("fork").Pool(len(names)) as pool:
+            new = pool.map(_run_big, names)
+        digests = {d["name"]: d for d in man.get("digests", [])}
+        digests.update({d["name"]: d for d in new})
+        man["digests"] = sorted(digests.values(), key=lambda d: d["name"])
+        json.dump(man, open(path, "w"), indent=1)
+        print("wrote", path)
+        return
     man["generator"] = "tests/golden/make_golden.py (reference delta_node/crypto/shamir loaded by file path)"
     man["python"] = sys.version.split()[0]
     t0 = time.time()
@@ -245,10 +280,7 @@ def main():
         digests[name] = d
         print(f"{name} done {time.time() - t0:.1f}s", flush=True)
     if args.big:
-        d = split_digest(3, 5, 1 << 24, 1, 1)
-        d["name"] = "split_t3n5_2e24"
-        digests[d["name"]] = d
-        print(f"2^24 done {time.time() - t0:.1f}s", flush=True)
+        digests["split_t3n5_2e24"] = _run_big("split_t3n5_2e24")
     man["digests"] = sorted(digests.values(), key=lambda d: d["name"])
     json.dump(man, open(path, "w"), indent=1)
     print("wrote", path)

@@ -74,3 +74,28 @@ def test_bench_rows_small():
     env_row = rows["share_envelope"]
     assert env_row["roundtrip_equal"] and env_row["oracle_prefix_equal"] and env_row["encrypt_kernel_equal_api"]
     assert rows["draw_split"]["equal_draw_then_split_and_state"]
+
+
+@pytest.mark.timeout(400)
+def test_bench_gpus_8_driver_command_rehearsal():
+    """The driver's N=8 command, rehearsed with 8 gloo ranks on the box's one
+    GPU at 2^20 elements: one JSON line with n_gpus 8, every rank's parity,
+    config 4's all-gather checked on every rank, and the reference CPU path
+    timed in the same run (cpu_baseline at every world size)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["DN_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--log2n", "20",
+                        "--config4", "1", "--config4-log2n", "20", "--rows", "0", "--config5", "0",
+                        "--cpu-budget", "2", "--steps", "4", "--warmup", "1", "--placements", "2"],
+                       capture_output=True, text=True, env=env, timeout=380)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8
+    assert line["config"]["elements_per_gpu"] == 1 << 17
+    assert line["parity"]["all_ranks_ok"] is True
+    assert line["config4"]["allgather"]["all_ranks_ok"] is True
+    cb = line["cpu_baseline"]
+    assert cb["run_at_world_size"] == 8 and cb["value"] > 0 and cb["cores"] == 1
+    assert cb["c_port"]["value"] > 0

@@ -327,7 +327,8 @@ def test_mt_state_in_place_matches_getstate():
     read exactly getstate()'s 624 words and index, a write through them is what
     getstate() then returns, and a random.Random subclass (the reference's
     SecretShare.random is one instance of the class) has the same offsets."""
-    assert _native._mt_layout(), "CPython's _random layout: the in-place path is the one this image runs"
+    if not _native._mt_layout():
+        pytest.skip("this interpreter's _random layout is not the checked one: the marshal path serves it")
 
     class Sub(random.Random):
         pass
@@ -346,3 +347,82 @@ def test_mt_state_in_place_matches_getstate():
         st[624] = 5
         assert list(rng.getstate()[1]) == st
     assert _native._mt_inplace(object()) is None
+
+
+def test_mt_marshal_path_matches_in_place(monkeypatch):
+    """With the in-place layout unavailable (another interpreter build), the
+    host draw marshals through getstate / setstate and ends in the same state
+    with the same coefficients as the in-place path."""
+    a, b = random.Random(5), random.Random(5)
+    want = _native.mt_draw_coeffs(a, 300, 2)
+    monkeypatch.setattr(_native, "_MT_LAYOUT", False)
+    assert _native._mt_inplace(b) is None
+    got = _native.mt_draw_coeffs(b, 300, 2)
+    assert np.array_equal(got, want) and a.getstate() == b.getstate()
+
+
+def test_mt_paths_only_for_plain_mt19937():
+    """The MT fast paths (jump-ahead, the state read in place) serve only a
+    random.Random whose draw methods are CPython's: SystemRandom (os.urandom)
+    and subclasses overriding randint / getrandbits / random are not MT19937
+    draws, so the vector API calls them per coefficient as the reference does
+    (shamir.py:59-61) — never reads their unused internal MT array."""
+    class Plain(random.Random):
+        pass
+
+    class Rec(random.Random):
+        def randint(self, a, b):
+            return 7
+
+    class Bits(random.Random):
+        def getrandbits(self, k):
+            return 3
+
+    assert _native.mt_compatible(random.Random(1)) and _native.mt_compatible(Plain(1))
+    for rng in (random.SystemRandom(), Rec(1), Bits(1), object()):
+        assert not _native.mt_compatible(rng)
+        assert _native._mt_inplace(rng) is None
+    # the generic draw is the reference's own per-coefficient call sequence
+    ss = shamir.SecretShare(3)
+    ss.random = Rec(1)
+    blk = shamir_mod._draw_coeffs_generic(ss.random, 5, 2)
+    assert [field.vec_to_ints(blk[j], 5) for j in range(2)] == [[7] * 5, [7] * 5]
+    r = random.Random(42)
+    blk = shamir_mod._draw_coeffs_generic(Plain(42), 4, 2)
+    want = [[r.randint(1, P - 1) for _ in range(2)] for _ in range(4)]
+    assert [field.vec_to_ints(blk[j], 4) for j in range(2)] == [[w[j] for w in want] for j in range(2)]
+    ss.random = random.SystemRandom()
+    with pytest.raises(NotImplementedError, match="sharded draw needs a plain random.Random"):
+        ss.draw_coeffs_vec(4, torch.device("cpu"), elem_offset=1, n_total=8)
+
+
+@pytest.mark.parametrize("coeffs,x,prime", [
+    ([5, 3, 2], 4, 101),                         # small prime
+    ([5, 3, 2], 0, P),                           # x = 0
+    ([123456789, 987654321, 5], 70000, P),       # x beyond the device range
+    (list(range(1, 101)), 7, P),                 # 100 coefficients
+    ([P + 5, -3, 2 * P - 1], 70001, P),          # unreduced and negative coefficients
+    ([10, -4, 7], -3, 2**127 - 1),               # negative x
+    ([10, 4, 7], 5, -13),                        # negative modulus (Python's sign of the divisor)
+    ([1 << 600, 3], 1 << 70, 2**61 - 1),         # wide operands
+    ([0, 0, 0], 12, 97),
+])
+def test_eval_at_any_integers_matches_reference_loop(coeffs, x, prime):
+    """_eval_at (shamir.py:19-25) outside the device split's range runs the
+    library's host Horner (dn_shamir_eval_at_host), equal to the reference's
+    Python loop for any integers (checked against oracle/py_shamir.eval_at's
+    restatement of that loop)."""
+    from oracle.py_shamir import eval_at as ref_eval_at
+
+    want = 0
+    for c in coeffs[::-1]:
+        want = (want * x + c) % prime
+    assert shamir_mod._eval_at(coeffs, x, prime) == want
+    if prime > 0:
+        assert ref_eval_at(coeffs, x, prime) == want
+
+
+def test_eval_at_edges():
+    assert shamir_mod._eval_at([], 5, 97) == 0
+    with pytest.raises(ZeroDivisionError):
+        shamir_mod._eval_at([1, 2], 3, 0)
