@@ -611,7 +611,10 @@ def rows_bench(dev, log2n: int) -> dict:
     # device-PRNG split (dn_m521_split_prng, SURVEY §8(d) config 2'): coefficients generated in-kernel
     from delta_node.crypto.shamir import _native as _nat
 
-    shs = [torch.empty((5, _field.vec_bytes(n)), dtype=torch.uint8, device=dev) for _ in range(3)]
+    from delta_node.crypto.shamir import memory as _memory
+
+    # make_shares_vec_prng's own output blocks (memory.share_block)
+    shs = [_memory.share_block((5, _field.vec_bytes(n)), dev) for _ in range(3)]
     sec = torch.from_numpy(secrets_int64(3, n)).to(dev)
     prng = {}
     # The rows before this one end in host-only work (the CPU baselines), and
@@ -751,14 +754,15 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
     import random
 
     from delta_node.crypto import shamir
-    from delta_node.crypto.shamir import _native, field
+    from delta_node.crypto.shamir import _native, field, memory
 
     n = 1 << log2n
     sec = torch.from_numpy(secrets_int64(5, n)).to(dev)
     # the fused call's generation writes the shares at the rate of their pages'
     # placement: three separately allocated outputs, the
     # best of `reps` calls on each, the median of the three quoted
-    outs = [torch.empty((5, field.vec_bytes(n)), dtype=torch.uint8, device=dev) for _ in range(3)]
+    # (the share blocks make_shares_vec allocates itself when out is None: memory.share_block)
+    outs = [memory.share_block((5, field.vec_bytes(n)), dev) for _ in range(3)]
     fused_by_buf, unfused = [], []
     ok = True
     wss = shamir.SecretShare(3)
@@ -969,7 +973,7 @@ def main():
     cdev = dev if not dist_on or torch.distributed.get_backend() == "nccl" else torch.device("cpu")
 
     from delta_node.crypto import shamir
-    from delta_node.crypto.shamir import _native, field
+    from delta_node.crypto.shamir import _native, field, memory
     from delta_node.crypto.shamir import dist as sdist
 
     N_total = 1 << args.log2n
@@ -1003,7 +1007,9 @@ def main():
     # a property of its share buffer's physical pages, so
     # the timed average is over several placements, not one allocation's.
     nbuf = max(1, args.placements)
-    share_bufs = [torch.empty((n, vb), dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+    # each the block make_shares_vec returns for out=None (memory.share_block:
+    # pooled 2 MiB physical chunks; torch.empty below 64 MiB)
+    share_bufs = [memory.share_block((n, vb), dev) for _ in range(nbuf)]
     rec = torch.empty(N, dtype=torch.int64, device=dev)
     w = _native.lagrange(xs, t)
     row_sets = [[sb[x - 1] for x in xs] for sb in share_bufs]
@@ -1148,7 +1154,9 @@ def main():
         "config": {"workload": f"{t}-of-{n} split + reconstruct(xs={xs}) of one 2^{args.log2n}-element int64 "
                                f"vector, GF(2^521-1), sharded by element over {world} GPU(s)",
                    "elements_total": N_total, "elements_per_gpu": N, "threshold": t, "shares": n, "xs": xs,
-                   "parallelism": f"element-shard x{world}"},
+                   "parallelism": f"element-shard x{world}",
+                   "share_blocks": "memory.share_block (make_shares_vec's own output allocation: pooled 2 MiB "
+                                   "physical chunks)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS,
                      # PMC bytes of the headline launch (2^24, 3-of-5) from the committed counter

@@ -1,41 +1,73 @@
-"""Opt-in share-block memory built from physical chunks (dn_block_alloc).
+"""Share-block memory built from 2 MiB physical chunks (dn_block_alloc).
 
-The split writes 330 B per element at 3-of-5 and its rate follows the
-physical pages of the share block.  `chunked_block` returns a
-uint8 device tensor whose memory is `chunk_bytes` physical chunks
-(hipMemCreate) mapped back to back — a composition the caller chooses instead
-of one allocation's luck.  Every API keeps accepting tensors from any
-allocator; this is only a way to get one.  The tensor owns the block: the
-memory is unmapped and released (after a device synchronise) when the last
-reference goes.
+The split writes 330 B per element at 3-of-5 (70 % of its traffic) and its
+rate follows the physical pages of the share block: a 5.5 GB
+block from one hipMalloc lands in a fast or a slow class (0.66 / 0.78 of
+8 TB/s for the split).  A block built from 2 MiB physical chunks mapped back to
+back (hipMemCreate / hipMemMap) ran in the fast class every time it was
+measured — 10 of 10 blocks at 0.786-0.800 against 6 of 10 torch.empty blocks
+(profiles/r04/a/block_probe.jsonl, and round 1's place_vmm2/3) — so the vector
+API allocates the share blocks it returns here (`share_block`), and callers
+may too.  Every API keeps accepting tensors from any allocator.
+
+Blocks are pooled: when the last tensor over a block goes, the block returns
+to an idle list (keyed by size, at most `POOL_IDLE_BYTES` held) and the next
+request of that size reuses it without new mappings; `empty_cache()` releases
+the idle blocks.  Below `CHUNKED_MIN_BYTES` (data that fits the caches, and
+where mapping costs more than it saves) `share_block` is torch.empty.
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Sequence, Union
+import math
+import threading
+from typing import Dict, List, Sequence, Tuple, Union
 
 from . import _native
 
-__all__ = ["chunked_block", "granularity"]
+__all__ = ["share_block", "chunked_block", "empty_cache", "granularity", "pool_stats"]
+
+CHUNK_BYTES = 2 << 20          # physical chunk of a pooled block
+CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
+POOL_IDLE_BYTES = 64 << 30     # most idle bytes the pool keeps mapped
+
+_lock = threading.Lock()
+_idle: Dict[Tuple[int, int, int], List[int]] = {}  # (device, nbytes, chunk) -> idle block pointers
+_idle_bytes = 0
+_stats = {"allocs": 0, "reuses": 0, "frees": 0}
+
+
+def _free_ptr(ptr: int) -> None:
+    _native.lib().dn_block_free(ptr)
+    _stats["frees"] += 1
 
 
 class _Block:
-    """A dn_block_alloc allocation seen through __cuda_array_interface__ (v3):
-    torch.as_tensor keeps this object alive as long as the tensor (its
-    deleter drops the reference), and __del__ frees the block."""
+    """One dn_block_alloc block seen through __cuda_array_interface__ (v3).
+    torch.as_tensor keeps this object alive as long as the tensor; when it
+    goes, the block returns to the idle pool (or is freed: pool full, or
+    pooled=False)."""
 
-    def __init__(self, nbytes: int, chunk_bytes: int, device: int, shape):
-        self._lib = _native.lib()
-        p = ctypes.c_void_p()
-        _native.check(self._lib.dn_block_alloc(nbytes, chunk_bytes, device, ctypes.byref(p)))
-        self.ptr = p.value
-        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "|u1", "data": (self.ptr, False),
+    def __init__(self, ptr: int, key: Tuple[int, int, int], shape, pooled: bool):
+        self.ptr, self.key, self.pooled = ptr, key, pooled
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "|u1", "data": (ptr, False),
                                          "version": 3, "strides": None}
 
     def __del__(self):
-        if getattr(self, "ptr", None):
-            self._lib.dn_block_free(self.ptr)
-            self.ptr = None
+        global _idle_bytes
+        ptr, self.ptr = getattr(self, "ptr", None), None
+        if not ptr:
+            return
+        try:
+            if self.pooled:
+                with _lock:
+                    if _idle_bytes + self.key[1] <= POOL_IDLE_BYTES:
+                        _idle.setdefault(self.key, []).append(ptr)
+                        _idle_bytes += self.key[1]
+                        return
+            _free_ptr(ptr)
+        except Exception:  # interpreter shutdown: the process releases the memory
+            pass
 
 
 def granularity(device: int = 0) -> int:
@@ -44,22 +76,74 @@ def granularity(device: int = 0) -> int:
     return g.value
 
 
-def chunked_block(shape: Union[int, Sequence[int]], chunk_bytes: int = 2 << 20, device=None):
-    """uint8 device tensor of `shape` whose memory is `chunk_bytes` physical
-    chunks mapped back to back (0: the library default, 2 MiB)."""
-    import math
-
+def _device_index(device):
     import torch
 
     dev = torch.device(device) if device is not None else _native.require_device()
     if dev.type != "cuda":
-        raise ValueError("chunked_block: a HIP device is required")
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        raise ValueError("share blocks live on a HIP device")
+    return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+
+
+def chunked_block(shape: Union[int, Sequence[int]], chunk_bytes: int = CHUNK_BYTES, device=None,
+                  pooled: bool = True):
+    """uint8 device tensor of `shape` whose memory is `chunk_bytes` physical
+    chunks mapped back to back (from the idle pool when one of this size is
+    there)."""
+    global _idle_bytes
+    import torch
+
+    dev = _device_index(device)
     shape = (int(shape),) if isinstance(shape, int) else tuple(int(s) for s in shape)
     nbytes = max(1, math.prod(shape))
-    blk = _Block(nbytes, int(chunk_bytes), idx, shape)
-    with torch.cuda.device(idx):
+    key = (dev.index, nbytes, int(chunk_bytes))
+    ptr = None
+    with _lock:
+        lst = _idle.get(key)
+        if lst:
+            ptr = lst.pop()
+            _idle_bytes -= nbytes
+            _stats["reuses"] += 1
+    if ptr is None:
+        p = ctypes.c_void_p()
+        rc = _native.lib().dn_block_alloc(nbytes, int(chunk_bytes), dev.index, ctypes.byref(p))
+        if rc:
+            empty_cache()  # idle blocks of other sizes may hold the memory
+            rc = _native.lib().dn_block_alloc(nbytes, int(chunk_bytes), dev.index, ctypes.byref(p))
+        _native.check(rc)
+        ptr = p.value
+        _stats["allocs"] += 1
+    blk = _Block(ptr, key, shape, pooled)
+    with torch.cuda.device(dev.index):
         t = torch.as_tensor(blk, device=dev)
-    if t.data_ptr() != blk.ptr or t.dtype != torch.uint8:
+    if t.data_ptr() != ptr or t.dtype != torch.uint8 or tuple(t.shape) != shape:
         raise RuntimeError("chunked_block: the tensor does not alias the block")
     return t
+
+
+def share_block(shape: Union[int, Sequence[int]], device=None):
+    """A share block (uint8 [n_shares, vec_bytes(n)] or any shape): pooled
+    2 MiB-chunk memory from CHUNKED_MIN_BYTES up, torch.empty below."""
+    import torch
+
+    dev = _device_index(device)
+    shape = (int(shape),) if isinstance(shape, int) else tuple(int(s) for s in shape)
+    if math.prod(shape) < CHUNKED_MIN_BYTES:
+        return torch.empty(shape, dtype=torch.uint8, device=dev)
+    return chunked_block(shape, CHUNK_BYTES, dev)
+
+
+def empty_cache() -> None:
+    """Release every idle pooled block (their memory returns to the device)."""
+    global _idle_bytes
+    with _lock:
+        ptrs = [p for lst in _idle.values() for p in lst]
+        _idle.clear()
+        _idle_bytes = 0
+    for p in ptrs:
+        _free_ptr(p)
+
+
+def pool_stats() -> dict:
+    with _lock:
+        return {**_stats, "idle_blocks": sum(len(v) for v in _idle.values()), "idle_bytes": _idle_bytes}

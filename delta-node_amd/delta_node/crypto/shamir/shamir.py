@@ -37,7 +37,7 @@ from functools import reduce
 from typing import List, Optional, Sequence, Tuple, Union
 
 from ... import serialize
-from . import _native, field, op
+from . import _native, field, memory, op
 
 __all__ = ["Share", "PRIME", "SecretShare"]
 
@@ -268,7 +268,8 @@ class SecretShare(object):
         values  int64 tensor [N] (any device; copied to the current HIP device)
         coeffs  optional uint8 device tensor [t-1, vec_bytes(N)]; default: drawn
                 from `self.random` as N sequential `make_shares` calls would
-        out     optional uint8 device tensor [shares, vec_bytes(N)]
+        out     optional uint8 device tensor [shares, vec_bytes(N)]; default: a
+                pooled block of 2 MiB physical chunks (memory.share_block)
         Returns uint8 device tensor [shares, vec_bytes(N)]: row x-1 holds share x
         of every element (tiled M521 layout, canonical residues).
         """
@@ -287,8 +288,8 @@ class SecretShare(object):
         n = vals.numel()
         t = max(self.threshold, 1)
         vb = field.vec_bytes(n)
-        if out is None:
-            out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
+        if out is None:  # pooled 2 MiB-chunk block (memory.py: the split's fast placement)
+            out = memory.share_block((max(shares, 0), vb), dev)
         elif (out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous()
               or out.device != dev):
             raise ValueError(f"make_shares_vec: out must be contiguous uint8 [{shares}, {vb}] on {dev}")
@@ -337,7 +338,7 @@ class SecretShare(object):
         n = vals.numel()
         vb = field.vec_bytes(n)
         if out is None:
-            out = torch.empty((max(shares, 0), vb), dtype=torch.uint8, device=dev)
+            out = memory.share_block((max(shares, 0), vb), dev)
         elif (out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous()
               or out.device != dev):
             raise ValueError(f"make_shares_vec_prng: out must be contiguous uint8 [{shares}, {vb}] on {dev}")
