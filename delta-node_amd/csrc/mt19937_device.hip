@@ -45,6 +45,7 @@ namespace {
 
 #include "mt19937_jump.inc"
 #include "mt19937_jump_short.inc"
+#include "mt19937_jump_direct.inc"
 
 // Substream lengths: L_k = 17 * 2^k words (2^k whole draws), k = 10, 12, 14,
 // one jump table each (rows A, C, B as in mt19937_jump.inc).  A draw of ncoef
@@ -52,11 +53,24 @@ namespace {
 // substreams for big draws (fewer jumps), short ones for small draws (a
 // substream's generation is one wave's sequential run: ~48 ns per draw, so
 // 2^14 draws cost ~0.8 ms whatever the vector size).
-constexpr int kMtLens = 3;
-constexpr int kMtLenLog2[kMtLens] = {10, 12, 14};
-__device__ const uint64_t kMtPolysDev[kMtLens][kMtJumpRows][kMtPolyWords] = {
+// Index 3 (2^8 draws) serves only draws of at most 65 substreams, whose
+// windows are all one jump from the caller's (direct rows D_s, below): it has
+// no A / C / B rows.
+constexpr int kMtLens = 4;
+constexpr int kMtLenLog2[kMtLens] = {10, 12, 14, 8};
+constexpr int kMtTabLens = 3;  // lengths with A / C / B rows
+__device__ const uint64_t kMtPolysDev[kMtTabLens][kMtJumpRows][kMtPolyWords] = {
     DN_MT_JUMP_POLYS_L10, DN_MT_JUMP_POLYS_L12, DN_MT_JUMP_POLYS};
 static_assert(kMtJumpL10 == 17ull << 10 && kMtJumpL12 == 17ull << 12 && kMtJumpL == 17ull << 14, "table lengths");
+// Direct rows (tools/gen_mt_jump.py --direct): D_s = x^(L - 624 + (s - 1) L),
+// W(s) = D_s(W_idx), s = 1..64, per length in kMtLenLog2's order.  A draw of
+// S <= 65 substreams takes ONE jump level from the caller's window instead of
+// A then B (one launch, one combine and one level's latency less).  Job poly
+// indices from kMtDirectBase address this table.
+__device__ const uint64_t kMtDirectDev[kMtLens][kMtDirectRows][kMtPolyWords] = {
+    DN_MT_JUMP_DIRECT_L10, DN_MT_JUMP_DIRECT_L12, DN_MT_JUMP_DIRECT_L14, DN_MT_JUMP_DIRECT_L8};
+static_assert(kMtJumpL8 == 17ull << 8, "table lengths");
+constexpr int32_t kMtDirectBase = kMtTabLens * kMtJumpRows;
 
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -65,10 +79,14 @@ constexpr int kMtN = 624, kMtM = 397;
 constexpr uint32_t kMtA = 0x9908b0dfu, kMtUp = 0x80000000u, kMtLo = 0x7fffffffu;
 
 // table index of the substream length of a draw of ncoef coefficients:
-// 2^14 draws from 2^24 coefficients, 2^12 from 2^21, else 2^10 (at least
-// ~2048 substreams for the big draws; a few hundred jumps and a short
-// generation run below)
-inline int mt_sub_len(uint64_t ncoef) { return ncoef >= (1ull << 24) ? 2 : ncoef >= (1ull << 21) ? 1 : 0; }
+// 2^14 draws from 2^24 coefficients, 2^12 from 2^21, 2^10 down to 65 * 2^8
+// + 1, else 2^8 (at least ~2048 substreams for the big draws; a few hundred
+// jumps and a short generation run below; the smallest draws: at most 65
+// substreams of 2^8 draws, one direct jump level and a ~4352-word run)
+inline int mt_sub_len(uint64_t ncoef) {
+  if (ncoef <= static_cast<uint64_t>(kMtDirectRows + 1) << 8) return 3;
+  return ncoef >= (1ull << 24) ? 2 : ncoef >= (1ull << 21) ? 1 : 0;
+}
 inline uint64_t mt_sub_draws(int ki) { return 1ull << kMtLenLog2[ki]; }
 
 __host__ __device__ inline uint32_t mt_temper(uint32_t y) {
@@ -317,7 +335,10 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   __syncthreads();
   if (j0 + wid >= a.njobs || dsti < 0) return;
 
-  const uint64_t* g = &kMtPolysDev[0][0][0] + static_cast<uint64_t>(poly) * kMtPolyWords;  // poly = table * rows + row
+  // poly = table * rows + row, or kMtDirectBase + length * 64 + s - 1 (wave-uniform)
+  const uint64_t* g = poly < kMtDirectBase
+                          ? &kMtPolysDev[0][0][0] + static_cast<uint64_t>(poly) * kMtPolyWords
+                          : &kMtDirectDev[0][0][0] + static_cast<uint64_t>(poly - kMtDirectBase) * kMtPolyWords;
   uint32_t Q[11];
 #pragma unroll
   for (int r = 0; r < 11; ++r) Q[r] = 0u;
@@ -966,6 +987,15 @@ void build_levels(uint64_t S, int ki, int back, Level lv[3]) {
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
   const int32_t prow0 = static_cast<int32_t>(S + 1);
+  if (last < static_cast<uint64_t>(kMtDirectRows)) {
+    // every window one jump from W_idx: W(s) = D_s(W_idx), one level
+    std::vector<std::pair<int32_t, int32_t>> pd;
+    for (uint64_t s = 1; s < S; ++s)
+      if (mt_window_needed(static_cast<uint32_t>(s), S, back))
+        pd.push_back({kMtDirectBase + ki * kMtDirectRows + static_cast<int32_t>(s - 1), static_cast<int32_t>(s)});
+    push_level(lv[0], {{-1, pd}}, prow0);
+    return;
+  }
   const int32_t t0 = ki * kMtJumpRows;  // the table's first row
   {
     std::vector<std::pair<int32_t, int32_t>> pd;
@@ -1019,7 +1049,10 @@ int mt_back() {
 
 MtHost& mt_levels(uint64_t S, int ki) {
   MtHost& H = tls_mt;
-  const int back = mt_back();
+  // 2^8-draw substreams run forward only: at t = 5 one holds a single
+  // emission group, and backward generation needs an even count (its window
+  // is the top of ring half 1); their one direct level takes the extra jumps
+  const int back = ki == 3 ? 0 : mt_back();
   const char* pb = tune_env("DN_MT_PARTS_B");
   const int parts_b = pb ? std::atoi(pb) : 0;
   if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b) {

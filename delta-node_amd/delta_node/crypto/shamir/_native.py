@@ -382,6 +382,24 @@ def mt_skip(rng, words: int) -> None:
     _mt_set_state(rng, version, gauss, state, index)
 
 
+_tls = threading.local()
+
+
+def _mt_scratch(nbytes: int, device):
+    """The device MT draw's scratch (job tables, windows), cached per thread
+    and device: every draw synchronises its stream before it returns, so the
+    thread's scratch is idle between its calls (no allocation per call)."""
+    import torch
+
+    cache = getattr(_tls, "scratch", None)
+    if cache is None:
+        cache = _tls.scratch = {}
+    buf = cache.get(device)
+    if buf is None or buf.numel() < nbytes:
+        cache[device] = buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+    return buf
+
+
 def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
     """`mt_draw_coeffs` with the coefficients generated on the GPU into `out`
     (uint8 device tensor [tm1, vec_bytes(n)]), bit-exact; `rng` advances
@@ -397,7 +415,7 @@ def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
         raise ValueError(f"mt_draw_coeffs_device: out must be a contiguous uint8 device tensor [{tm1}, {vb}]")
     L = lib()
     sb = int(L.dn_mt19937_device_scratch_bytes(n, tm1))
-    scratch = torch.empty(sb, dtype=torch.uint8, device=out.device)
+    scratch = _mt_scratch(sb, out.device)
     ip = _mt_inplace(rng)  # the entry point writes the state only on success
     if ip:
         rc = L.dn_mt19937_draw_coeffs_device(ip[0], ip[1], n, tm1, out.data_ptr(), scratch.data_ptr(), sb,
@@ -431,7 +449,7 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
         if not x.is_cuda or x.device != shares.device or not x.is_contiguous():
             raise ValueError(f"mt_split_device: {name} must be a contiguous tensor on the shares' HIP device")
     sb = int(L.dn_mt19937_device_scratch_bytes(n, t - 1))
-    scratch = torch.empty(sb, dtype=torch.uint8, device=shares.device)
+    scratch = _mt_scratch(sb, shares.device)
     ip = _mt_inplace(rng)  # the entry point writes the state only on success
     if ip:
         rc = L.dn_mt19937_split_device(ip[0], ip[1], secrets.data_ptr(), shares.data_ptr(), n, t, n_shares,

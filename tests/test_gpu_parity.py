@@ -403,8 +403,28 @@ def test_device_mt_draw_equals_host_draw_past_4096_substreams():
     assert a.getstate() == b.getstate()
 
 
+@pytest.mark.parametrize("n,tm1,pre", [(8320, 2, 0), (8321, 2, 600), (4160, 4, 17), (16640, 1, 1), (16641, 1, 0),
+                                       (33280, 2, 623), (33281, 2, 5), (1 << 16, 2, 9)])
+def test_device_mt_draw_direct_level_boundaries(n, tm1, pre):
+    """Draws of at most 65 substreams take ONE jump level from the caller's
+    window (direct rows D_s = x^(L - 624 + (s-1) L)): 2^8-draw substreams up to
+    65 * 2^8 coefficients (forward generation only), 2^10-draw substreams up
+    to 65 * 2^10, two levels (A then B) above.  Each side of both boundaries
+    equals the host draw byte for byte, same final state."""
+    a = random.Random(n * 3 + tm1)
+    if pre:
+        a.getrandbits(32 * pre)
+    b = random.Random()
+    b.setstate(a.getstate())
+    want = _native.mt_draw_coeffs(a, n, tm1)
+    got = torch.zeros((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    assert _native.mt_draw_coeffs_device(b, n, tm1, got)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert a.getstate() == b.getstate()
+
+
 @pytest.mark.parametrize("t,n", [(2, 3), (3, 5), (5, 9), (3, 200)])
-@pytest.mark.parametrize("N", [1, 63, 257, 1000, 8192 + 5, (1 << 20) + 77])
+@pytest.mark.parametrize("N", [1, 63, 257, 1000, 4160, 8192 + 5, 8320, 33280, (1 << 20) + 77])
 def test_fused_draw_split_equals_draw_then_split(t, n, N):
     """make_shares_vec with the reference's coefficients takes the fused
     device path (dn_mt19937_split_device: the MT19937 draws feed the split in

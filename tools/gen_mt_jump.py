@@ -238,10 +238,50 @@ def main_short(out_path):
     print("wrote", out_path)
 
 
+def direct_polys(P, l_words, rows=RADIX):
+    """D_s = x^(L - 624 + (s - 1) L), s = 1..rows: window s straight from W_idx
+    (one jump level for draws of at most rows + 1 substreams), checked."""
+    red = Reducer(P)
+    xL = xpow(l_words, P)
+    g = xpow(l_words - N, P)
+    polys = []
+    for s in range(1, rows + 1):
+        polys.append((f"D{s}", l_words - N + (s - 1) * l_words, g))
+        g = red(clmul(g, xL))
+    for name, J, gp in polys[::17] + polys[-1:]:
+        assert gp == xpow(J, P), name
+    w0 = list(random.Random(7).getstate()[1][:N])
+    for name, J, gp in polys[:2]:  # the two smallest against plain stepping
+        a = jump(w0, gp)
+        b = w0
+        for _ in range(J):
+            b = step(b)
+        assert a[1:] == b[1:] and (a[0] ^ b[0]) >> 31 == 0, name
+    return polys
+
+
+def main_direct(out_path):
+    """Direct rows D_1..D_64 for the four substream lengths of the device draw
+    (17 * 2^k words, k = 10, 12, 14 and 8, in the device's table order): a
+    draw of S <= 65 substreams reaches every window in ONE jump level."""
+    P = char_poly()
+    with open(out_path, "w") as f:
+        f.write("// Generated by tools/gen_mt_jump.py --direct — do not edit.\n")
+        f.write("// Direct jump rows D_s = x^(L - 624 + (s - 1) L) mod P, s = 1..64 (row s - 1):\n")
+        f.write("// W(s) = D_s(W_idx), for substreams of L = 17 * 2^k words, k = 10, 12, 14, 8.\n")
+        f.write("constexpr int kMtDirectRows = 64;\n")
+        f.write("constexpr uint64_t kMtJumpL8 = 4352ull;\n")
+        for k in (10, 12, 14, 8):
+            write_polys(f, f"DN_MT_JUMP_DIRECT_L{k}", direct_polys(P, 17 * (1 << k)))
+    print("wrote", out_path)
+
+
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     csrc = os.path.join(root, "delta-node_amd", "csrc")
-    if len(sys.argv) > 1 and sys.argv[1] == "--short":
+    if len(sys.argv) > 1 and sys.argv[1] == "--direct":
+        main_direct(sys.argv[2] if len(sys.argv) > 2 else os.path.join(csrc, "mt19937_jump_direct.inc"))
+    elif len(sys.argv) > 1 and sys.argv[1] == "--short":
         main_short(sys.argv[2] if len(sys.argv) > 2 else os.path.join(csrc, "mt19937_jump_short.inc"))
     else:
         main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(csrc, "mt19937_jump.inc"))

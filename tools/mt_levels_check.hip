@@ -1,7 +1,7 @@
 // mt_levels_check.hip — host check of the MT19937 device draw's jump-job
 // builder (build_levels / push_level in delta-node_amd/csrc/mt19937_device.hip,
 // included here; no GPU needed): for substream counts S up to 300 and the
-// boundary sizes up to 65537, for all three substream lengths and both
+// boundary sizes up to 65537, for all four substream lengths (2^8 draws: direct levels only) and both
 // generation modes, every window a generation wave starts from (1 .. S-1, or
 // with backward generation the odd ones and S-1: mt_sub_forward) is produced
 // exactly once (by a whole jump, or by the XOR of its parts) and no other
@@ -21,6 +21,7 @@ void mt_advance_window(const uint32_t*, uint64_t, uint32_t*) {} }
 using namespace dn;
 extern "C" uint64_t dn_m521_vec_bytes(uint64_t n) { return n; }
 int check(uint64_t S, int ki, int back) {
+  const bool direct = S - 1 <= static_cast<uint64_t>(kMtDirectRows);
   Level LV[3];
   build_levels(S, ki, back, LV);
   std::vector<const Level*> lv = {&LV[0], &LV[1], &LV[2]};
@@ -40,7 +41,14 @@ int check(uint64_t S, int ki, int back) {
         if (j.dst < 0) continue;
         if (j.src >= 0 && !known[j.src]) { printf("S=%llu lvl %d src %d unknown\n", (unsigned long long)S, k, j.src); return 1; }
         const int lo = j.span & 0xffff, hi = j.span >> 16;
-        if (j.poly < ki * kMtJumpRows || j.poly >= (ki + 1) * kMtJumpRows) bad++;
+        if (direct) {  // one level from W_idx, rows D_s of this length
+          if (k != 0 || j.src != -1 || j.poly < kMtDirectBase + ki * kMtDirectRows ||
+              j.poly >= kMtDirectBase + (ki + 1) * kMtDirectRows)
+            bad++;
+          if (L.comb.empty() && j.poly != kMtDirectBase + ki * kMtDirectRows + j.dst - 1) bad++;  // W(s) <- D_s
+        } else if (ki >= kMtTabLens || j.poly < ki * kMtJumpRows || j.poly >= (ki + 1) * kMtJumpRows) {
+          bad++;
+        }
         if (L.comb.empty()) {
           if (lo != 0 || hi != kMtPolyWords) bad++;
           if (j.dst < 1 || (uint64_t)j.dst >= S || known[j.dst]) { printf("dst %d\n", j.dst); bad++; }
@@ -64,6 +72,7 @@ int check(uint64_t S, int ki, int back) {
         partw.erase(it);
       }
       if (expect_lo != kMtPolyWords) bad++;
+      if (direct && poly != kMtDirectBase + ki * kMtDirectRows + c.dst - 1) bad++;  // W(s) <- D_s
       known[c.dst] = 2;
     }
     if (!partw.empty()) bad++;
@@ -81,7 +90,10 @@ int main() {
   for (uint64_t S : {511ull, 512ull, 513ull, 1024ull, 1025ull, 2047ull, 2048ull, 2049ull, 4095ull, 4096ull, 4097ull, 4098ull, 5000ull, 8193ull, 16385ull, 20000ull, 65537ull})
     Ss.push_back(S);
   for (uint64_t S : Ss)
-    for (int ki = 0; ki < 3; ++ki) fails += check(S, ki, 0) + check(S, ki, 1);
+    for (int ki = 0; ki < kMtLens; ++ki) {
+      if (ki >= kMtTabLens && S - 1 > static_cast<uint64_t>(kMtDirectRows)) continue;  // direct-only length
+      fails += check(S, ki, 0) + check(S, ki, 1);
+    }
   // summary for a few sizes
   for (uint64_t S : {2ull, 129ull, 513ull, 2049ull, 4097ull, 16385ull}) {
     Level L[3]; build_levels(S, 2, 1, L);
