@@ -1129,10 +1129,43 @@ struct PinLease {
   PinLease& operator=(const PinLease&) = delete;
 };
 
-constexpr uint64_t kHead = 4096;  // flag (4 B at 0), final array (2496 B at 256)
+constexpr uint64_t kHead = 2816;  // flag (4 B at 0), final array (2496 B at 256), pad to 256 B
 
-// words the job tables take in the scratch, rounded up to 256 B
-inline uint64_t mt_jobs_pad(const MtHost& H) { return (H.jobs.size() + 63) / 64 * 64; }
+// The levels' job tables on the device, one upload per (device, shape): they
+// depend on (S, ki, back, parts) only, so a call copies just its own state
+// (head, W_idx, row 0: ~7.8 KB — a blit, where the job tables of a large draw
+// went by SDMA and the first jump waited ~11-14 us on its completion signal;
+// profiles/r04/c/msv_timeline.json).  Library-owned, never freed (a few KB to
+// ~100 KB per shape; the runtime may be torn down before static destructors).
+struct DevJobs {
+  int dev;
+  uint64_t S;
+  int ki, back, parts_b;
+  void* p;
+};
+
+const void* device_jobs(const MtHost& H, int* err) {
+  static std::mutex* m = new std::mutex;
+  static auto* cache = new std::vector<DevJobs>;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    *err = 1;
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(*m);
+  for (const DevJobs& d : *cache)
+    if (d.dev == dev && d.S == H.S && d.ki == H.ki && d.back == H.back && d.parts_b == H.parts_b) return d.p;
+  void* p = nullptr;
+  const size_t bytes = std::max<size_t>(H.jobs.size() * 4, 16);
+  if (hipMalloc(&p, bytes) != hipSuccess ||
+      (!H.jobs.empty() && hipMemcpy(p, H.jobs.data(), H.jobs.size() * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+    if (p) (void)hipFree(p);
+    *err = 1;
+    return nullptr;
+  }
+  cache->push_back({dev, H.S, H.ki, H.back, H.parts_b, p});
+  return p;
+}
 
 }  // namespace
 }  // namespace dn
@@ -1144,7 +1177,7 @@ extern "C" uint64_t dn_mt19937_device_scratch_bytes(uint64_t n_elem, int tm1) {
   const uint64_t S = ncoef ? mt_subs(ncoef) : 0;
   if (!S) return kHead + kMtN * 4;
   const MtHost& H = mt_levels(S, mt_sub_len(ncoef));
-  return kHead + mt_jobs_pad(H) * 4 + (1 + S + 1 + H.part_rows) * kMtN * 4;
+  return kHead + (1 + S + 1 + H.part_rows) * kMtN * 4;
 }
 
 namespace dn {
@@ -1185,30 +1218,33 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     fidx = static_cast<int32_t>(m_end - kMtN * (q - 1));
   }
 
-  // scratch: head (flag at 0, final array at 256) | jump jobs, combine jobs
-  // (padded to 256 B) | W_idx (the caller's array advanced idx words: window
-  // "-1", the level-A source) | windows 0..S (row 0 the caller's array; row S
-  // unused) | part rows (split levels).  Everything the GPU needs from the host
-  // is the prefix head .. row 0: ONE copy from the pinned staging buffer,
-  // which holds that prefix and, in its tail, the head read back at the end.
+  // scratch: head (flag at 0, final array at 256) | W_idx (the caller's
+  // array advanced idx words: window "-1", the level-A source) | windows 0..S
+  // (row 0 the caller's array; row S unused) | part rows (split levels).  The
+  // job tables are the device copy of this shape's (device_jobs).  What the
+  // GPU needs from the host is the prefix head .. row 0: ONE copy from the
+  // pinned staging buffer, which holds that prefix and, in its tail, the head
+  // read back at the end.
   const int ki = mt_sub_len(ncoef);
   MtHost& H = mt_levels(S, ki);
   const Level* lv = H.lv;
   const uint64_t njobs = lv[0].jobs.size() + lv[1].jobs.size() + lv[2].jobs.size();
-  const size_t wj = mt_jobs_pad(H), wpre = kHead / 4 + wj + 2 * kMtN, wh = 256 / 4 + kMtN;
+  int jerr = 0;
+  const void* jobs_dev = device_jobs(H, &jerr);
+  if (jerr) return set_error(DN_ERR_HIP, "%s: job tables on the device", name);
+  const size_t wpre = kHead / 4 + 2 * kMtN, wh = 256 / 4 + kMtN;
   PinLease lease(wpre + wh);  // idle again once this call has synchronised its stream
   uint32_t* pin = lease.p;
   if (!pin) return set_error(DN_ERR_HIP, "%s: pinned staging buffer", name);
-  uint32_t *stj = pin + kHead / 4, *stw = stj + wj, *head = pin + wpre;
-  std::memset(pin, 0, kHead);
-  if (!H.jobs.empty()) std::memcpy(stj, H.jobs.data(), H.jobs.size() * 4);
+  uint32_t *stw = pin + kHead / 4, *head = pin + wpre;
+  std::memset(pin, 0, 256);  // the flag (the final array is written by the device)
   mt_advance_window(mt_state, static_cast<uint64_t>(idx), stw);  // W_idx
   std::memcpy(stw + kMtN, mt_state, kMtN * 4);                    // row 0
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint8_t* sc = static_cast<uint8_t*>(scratch);
-  JumpJob* djobs = reinterpret_cast<JumpJob*>(sc + kHead);
-  CombineJob* dcomb = reinterpret_cast<CombineJob*>(djobs + njobs);
-  uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead) + wj + kMtN;  // row 0
+  const JumpJob* djobs = static_cast<const JumpJob*>(jobs_dev);
+  const CombineJob* dcomb = reinterpret_cast<const CombineJob*>(djobs + njobs);
+  uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead) + kMtN;  // row 0
   hipError_t err = hipMemcpyAsync(sc, pin, wpre * 4, hipMemcpyHostToDevice, s);
   if (err != hipSuccess) {
     (void)hipStreamSynchronize(s);  // the staging buffer is reused by the next call
