@@ -186,7 +186,10 @@ constexpr int kEPair = 16 * kEVWords + 2;              // 2050 words
 constexpr int kEWrap = ((5 * kEPair + 63) / 64) * 64;  // 10304 words
 constexpr int kEWords = kEWrap + 5 * kEPair;           // 82 KB
 constexpr int kJumpWaves = 16;  // at most this many jumps (waves) per workgroup, all from one source and part
-constexpr int kMaxParts = 16;   // at most this many parts per jump
+#ifndef DN_MT_MAX_PARTS
+#define DN_MT_MAX_PARTS 16
+#endif
+constexpr int kMaxParts = DN_MT_MAX_PARTS;  // at most this many parts per jump
 
 // a ^ b ^ c in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96;
 // hipcc keeps two v_xor_b32 otherwise)
@@ -1305,7 +1308,10 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   return DN_OK;
 }
 
-constexpr int kSc1 = 16;  // buffer-store cache policy: sc1
+#ifndef DN_MT_SAUX
+#define DN_MT_SAUX 16
+#endif
+constexpr int kSc1 = DN_MT_SAUX;  // buffer-store cache policy of the 3-of-5 share stores: sc1 (16)
 
 template <int T>
 void launch_gen(GenArgs& ga, hipStream_t s) {

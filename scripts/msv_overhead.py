@@ -33,3 +33,30 @@ for lg in (8, 12, 16, 20, 24):
     torch.cuda.synchronize()
     out[f"2^{lg}"] = (time.perf_counter() - t0) / reps * 1e3
 print(json.dumps({"make_shares_vec_ms_per_call": out}))
+
+# the same 2^12 call through the C-ABI directly (arguments prepared once):
+# the difference to make_shares_vec is the binding's Python time per call
+from delta_node.crypto.shamir import _native  # noqa: E402
+
+N = 1 << 12
+sec = torch.randint(-(1 << 62), 1 << 62, (N,), dtype=torch.int64, device=dev)
+sh = torch.empty((5, field.vec_bytes(N)), dtype=torch.uint8, device=dev)
+ss = shamir.SecretShare(3)
+ss.random.seed(12)
+L = _native.lib()
+sb = int(L.dn_mt19937_device_scratch_bytes(N, 2))
+scratch = torch.empty(sb, dtype=torch.uint8, device=dev)
+ip = _native._mt_inplace(ss.random)
+args = (ip[0], ip[1], sec.data_ptr(), sh.data_ptr(), N, 3, 5, scratch.data_ptr(), sb, _native.stream_ptr())
+for _ in range(5):
+    assert L.dn_mt19937_split_device(*args) == 0
+reps = 200
+t0 = time.perf_counter()
+for _ in range(reps):
+    L.dn_mt19937_split_device(*args)
+raw = (time.perf_counter() - t0) / reps * 1e3
+t0 = time.perf_counter()
+for _ in range(reps):
+    ss.make_shares_vec(sec, 5, out=sh)
+api = (time.perf_counter() - t0) / reps * 1e3
+print(json.dumps({"2^12_raw_c_abi_ms": raw, "2^12_make_shares_vec_ms": api}))
