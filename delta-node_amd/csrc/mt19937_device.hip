@@ -186,8 +186,11 @@ constexpr int kEPair = 16 * kEVWords + 2;              // 2050 words
 constexpr int kEWrap = ((5 * kEPair + 63) / 64) * 64;  // 10304 words
 constexpr int kEWords = kEWrap + 5 * kEPair;           // 82 KB
 constexpr int kJumpWaves = 16;  // at most this many jumps (waves) per workgroup, all from one source and part
+// 32: small levels (the direct level of a small draw, level A) split into
+// parts of ~10 Horner steps (make_shares_vec 2^12 -1.5 us, level A 26.5 vs
+// 29.1 us at 2^24; profiles/r04/e/)
 #ifndef DN_MT_MAX_PARTS
-#define DN_MT_MAX_PARTS 16
+#define DN_MT_MAX_PARTS 32
 #endif
 constexpr int kMaxParts = DN_MT_MAX_PARTS;  // at most this many parts per jump
 
@@ -608,6 +611,11 @@ __device__ __forceinline__ void back_run(uint32_t* Rg, uint32_t M, uint32_t& top
   if constexpr (NB % 6) back_batch<NB % 6>(Rg, M, top, lane);
 }
 
+// A rejected draw: every writer stores the same nonzero word, so a plain
+// store serves (no atomic: the flag may live in pinned host memory, where a
+// device atomic would be a PCIe atomic).
+__device__ __forceinline__ void mt_flag(const GenArgs& a) { __hip_atomic_store(a.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+
 // 64 draws of one group (lane = draw c of this substream, raw words 17 c ..
 // 17 c + 16 of the group at `rb`): temper, +1, rejection test, tiled store.
 __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb, uint64_t qb, uint32_t rbm,
@@ -621,7 +629,7 @@ __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb,
   uint32_t all = v[1];
 #pragma unroll
   for (int i = 2; i < 16; ++i) all &= v[i];
-  if (v[16] == 0x1FFu && v[0] >= 0xFFFFFFFEu && all == 0xFFFFFFFFu) atomicOr(a.flag, 1u);  // >= p - 1: rejected
+  if (v[16] == 0x1FFu && v[0] >= 0xFFFFFFFEu && all == 0xFFFFFFFFu) mt_flag(a);  // >= p - 1: rejected
   uint32_t cy = 1u;  // + 1 (randint's lower bound); v < p - 1: no carry out of limb 16
 #pragma unroll
   for (int i = 0; i < kLimbs; ++i) v[i] = __builtin_addc(v[i], 0u, cy, &cy);
@@ -675,7 +683,7 @@ __device__ __forceinline__ void emit_prepare(const GenArgs& a, const uint32_t* r
     uint32_t all = c[j][1];
 #pragma unroll
     for (int i = 2; i < 16; ++i) all &= c[j][i];
-    if (c[j][16] == 0x1FFu && c[j][0] >= 0xFFFFFFFEu && all == 0xFFFFFFFFu) atomicOr(a.flag, 1u);
+    if (c[j][16] == 0x1FFu && c[j][0] >= 0xFFFFFFFEu && all == 0xFFFFFFFFu) mt_flag(a);
     uint32_t cy = 1u;  // randint(1, p-1) = 1 + getrandbits(521)
 #pragma unroll
     for (int i = 0; i < kLimbs; ++i) c[j][i] = __builtin_addc(c[j][i], 0u, cy, &cy);
@@ -1134,6 +1142,15 @@ struct PinLease {
 
 constexpr uint64_t kHead = 2816;  // flag (4 B at 0), final array (2496 B at 256), pad to 256 B
 
+// DN_MT_HOST_HEAD = 1: the generation writes the flag and CPython's final
+// array straight into the call's pinned staging buffer (mapped host memory,
+// visible once the stream has synchronised) instead of the scratch head and
+// a device-to-host copy after it.
+// (make_shares_vec 2^12 -1.5 us: no read-back copy; profiles/r04/e/)
+#ifndef DN_MT_HOST_HEAD
+#define DN_MT_HOST_HEAD 1
+#endif
+
 // The levels' job tables on the device, one upload per (device, shape): they
 // depend on (S, ki, back, parts) only, so a call copies just its own state
 // (head, W_idx, row 0: ~7.8 KB — a blit, where the job tables of a large draw
@@ -1272,8 +1289,19 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   }
   GenArgs ga{};
   ga.wins = dwin;
+#if DN_MT_HOST_HEAD
+  head[0] = 0u;  // the flag; the final-state wave writes the final array at head + 64
+  void* dhead = nullptr;
+  if (hipHostGetDevicePointer(&dhead, head, 0) != hipSuccess || !dhead) {
+    (void)hipStreamSynchronize(s);
+    return set_error(DN_ERR_HIP, "%s: staging buffer not mapped", name);
+  }
+  ga.flag = static_cast<uint32_t*>(dhead);
+  ga.fin = static_cast<uint32_t*>(dhead) + 64;
+#else
   ga.flag = reinterpret_cast<uint32_t*>(sc);
   ga.fin = reinterpret_cast<uint32_t*>(sc + 256);
+#endif
   ga.ncoef = ncoef;
   ga.sub_draws = mt_sub_draws(ki);
   ga.vb = dn_m521_vec_bytes(n_elem);
@@ -1295,7 +1323,9 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     return set_error(DN_ERR_HIP, "%s: launch: %s", name, hipGetErrorString(err));
   }
 
+#if !DN_MT_HOST_HEAD
   err = hipMemcpyAsync(head, sc, wh * 4, hipMemcpyDeviceToHost, s);  // flag .. final array
+#endif
   const hipError_t serr = hipStreamSynchronize(s);
   if (err == hipSuccess) err = serr;
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));

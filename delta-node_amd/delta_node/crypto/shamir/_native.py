@@ -138,11 +138,9 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_mt19937_device_scratch_bytes.restype = u64
     L.dn_mt19937_device_scratch_bytes.argtypes = [u64, i32]
     L.dn_mt19937_draw_coeffs_device.restype = i32
-    L.dn_mt19937_draw_coeffs_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
-                                                u64, i32, vp, vp, u64, vp]
+    L.dn_mt19937_draw_coeffs_device.argtypes = [vp, vp, u64, i32, vp, vp, u64, vp]  # state, index by address
     L.dn_mt19937_split_device.restype = i32
-    L.dn_mt19937_split_device.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32), vp, vp, u64,
-                                          i32, i32, vp, u64, vp]
+    L.dn_mt19937_split_device.argtypes = [vp, vp, vp, vp, u64, i32, i32, vp, u64, vp]
     L.dn_mt19937_split_supported.restype = i32
     L.dn_mt19937_split_supported.argtypes = [u64, i32, i32]
     L.dn_shamir_make_shares_host.restype = i32
@@ -195,19 +193,26 @@ def check(rc: int) -> None:
 
 
 # ------------------------------------------------------------------ device
+_HAS_DEVICE = False  # a HIP device has been seen (it does not go away)
+
+
 def require_device():
     """The current HIP device; raise if there is none (no CPU fallback)."""
+    global _HAS_DEVICE
     import torch
 
-    if not torch.cuda.is_available():
-        raise RuntimeError("delta_node.crypto.shamir: no HIP device visible; the MI355X path has no CPU fallback")
+    if not _HAS_DEVICE:
+        if not torch.cuda.is_available():
+            raise RuntimeError("delta_node.crypto.shamir: no HIP device visible; the MI355X path has no CPU fallback")
+        _HAS_DEVICE = True
     return torch.device("cuda", torch.cuda.current_device())
 
 
 def stream_ptr() -> int:
+    """The current device's current stream (hipStream_t as an int)."""
     import torch
 
-    return torch.cuda.current_stream().cuda_stream
+    return torch._C._cuda_getCurrentRawStream(torch.cuda.current_device())
 
 
 def _ptr(t) -> Optional[int]:
@@ -353,17 +358,23 @@ def _mt_layout():
 _MT_METHODS = ("randint", "randrange", "_randbelow", "getrandbits", "random", "getstate", "setstate", "seed")
 
 
+_MT_CLASS_OK = {}  # class -> mt_compatible verdict (classes are not re-patched at run time)
+
+
 def mt_compatible(rng) -> bool:
     """True when `rng.randint` is CPython's MT19937 draw: a random.Random
     whose class overrides none of the methods the draw goes through.  Only
     then may the device / host MT paths (jump-ahead, the caller's state read
     directly) replace the reference's per-coefficient calls."""
-    import random as _rnd
-
-    if not isinstance(rng, _rnd.Random):
-        return False
     cls = type(rng)
-    return all(getattr(cls, m, None) is getattr(_rnd.Random, m) for m in _MT_METHODS)
+    ok = _MT_CLASS_OK.get(cls)
+    if ok is None:
+        import random as _rnd
+
+        ok = issubclass(cls, _rnd.Random) and all(getattr(cls, m, None) is getattr(_rnd.Random, m)
+                                                  for m in _MT_METHODS)
+        _MT_CLASS_OK[cls] = ok
+    return ok
 
 
 def _mt_inplace(rng):
@@ -373,6 +384,14 @@ def _mt_inplace(rng):
         return None
     return (ctypes.cast(id(rng) + lay[1], ctypes.POINTER(ctypes.c_uint32)),
             ctypes.cast(id(rng) + lay[0], ctypes.POINTER(ctypes.c_int32)))
+
+
+def _mt_inplace_addr(rng):
+    """(state address, index address) inside rng's own MT19937 state, or None."""
+    lay = _mt_layout()
+    if not lay or not mt_compatible(rng):
+        return None
+    return id(rng) + lay[1], id(rng) + lay[0]
 
 
 def mt_skip(rng, words: int) -> None:
@@ -416,14 +435,14 @@ def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
     L = lib()
     sb = int(L.dn_mt19937_device_scratch_bytes(n, tm1))
     scratch = _mt_scratch(sb, out.device)
-    ip = _mt_inplace(rng)  # the entry point writes the state only on success
+    ip = _mt_inplace_addr(rng)  # the entry point writes the state only on success
     if ip:
         rc = L.dn_mt19937_draw_coeffs_device(ip[0], ip[1], n, tm1, out.data_ptr(), scratch.data_ptr(), sb,
                                              stream_ptr())
     else:
         version, gauss, state, index = _mt_state(rng)
-        rc = L.dn_mt19937_draw_coeffs_device(state, ctypes.byref(index), n, tm1, out.data_ptr(), scratch.data_ptr(),
-                                             sb, stream_ptr())
+        rc = L.dn_mt19937_draw_coeffs_device(ctypes.addressof(state), ctypes.addressof(index), n, tm1,
+                                             out.data_ptr(), scratch.data_ptr(), sb, stream_ptr())
     if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
         return False
     check(rc)
@@ -450,14 +469,14 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
             raise ValueError(f"mt_split_device: {name} must be a contiguous tensor on the shares' HIP device")
     sb = int(L.dn_mt19937_device_scratch_bytes(n, t - 1))
     scratch = _mt_scratch(sb, shares.device)
-    ip = _mt_inplace(rng)  # the entry point writes the state only on success
+    ip = _mt_inplace_addr(rng)  # the entry point writes the state only on success
     if ip:
         rc = L.dn_mt19937_split_device(ip[0], ip[1], secrets.data_ptr(), shares.data_ptr(), n, t, n_shares,
                                        scratch.data_ptr(), sb, stream_ptr())
     else:
         version, gauss, state, index = _mt_state(rng)
-        rc = L.dn_mt19937_split_device(state, ctypes.byref(index), secrets.data_ptr(), shares.data_ptr(), n, t,
-                                       n_shares, scratch.data_ptr(), sb, stream_ptr())
+        rc = L.dn_mt19937_split_device(ctypes.addressof(state), ctypes.addressof(index), secrets.data_ptr(),
+                                       shares.data_ptr(), n, t, n_shares, scratch.data_ptr(), sb, stream_ptr())
     if rc in (DN_ERR_RETRY, DN_ERR_UNSUPPORTED):
         return False
     check(rc)

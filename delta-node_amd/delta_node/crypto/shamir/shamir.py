@@ -75,6 +75,20 @@ def _to_device_vecs(ints: Sequence[int], dev):
     return torch.from_numpy(host).to(dev)
 
 
+def _device_values(values, dev, name: str):
+    """`values` as a contiguous 1-D int64 tensor on `dev` (no conversion when
+    it already is one: the common call, a resident vector)."""
+    import torch
+
+    if (isinstance(values, torch.Tensor) and values.device == dev and values.dtype == torch.int64
+            and values.dim() == 1 and values.is_contiguous()):
+        return values
+    vals = torch.as_tensor(values)
+    if vals.dtype not in (torch.int64, torch.uint64):
+        raise TypeError(f"{name}: values must be an int64 tensor")
+    return vals.reshape(-1).to(dev).contiguous()
+
+
 def _eval_many(coeffs: Sequence[int], n_shares: int) -> List[int]:
     """y(x) = sum_j coeffs[j] x^j mod p for x = 1..n_shares, on the GPU.
     coeffs[0] is the secret (any size; reduced mod p here)."""
@@ -281,10 +295,7 @@ class SecretShare(object):
         if shares > _native.MAX_SHARES or self.threshold > _native.MAX_THRESHOLD:
             raise NotImplementedError("make_shares_vec: at most 65535 shares and threshold 64")
         dev = _device()
-        vals = torch.as_tensor(values)
-        if vals.dtype not in (torch.int64, torch.uint64):
-            raise TypeError("make_shares_vec: values must be an int64 tensor")
-        vals = vals.reshape(-1).to(dev).contiguous()
+        vals = _device_values(values, dev, "make_shares_vec")
         n = vals.numel()
         t = max(self.threshold, 1)
         vb = field.vec_bytes(n)
@@ -331,10 +342,7 @@ class SecretShare(object):
         if key is None:
             key = _secrets.token_bytes(32)
         dev = _device()
-        vals = torch.as_tensor(values)
-        if vals.dtype not in (torch.int64, torch.uint64):
-            raise TypeError("make_shares_vec_prng: values must be an int64 tensor")
-        vals = vals.reshape(-1).to(dev).contiguous()
+        vals = _device_values(values, dev, "make_shares_vec_prng")
         n = vals.numel()
         vb = field.vec_bytes(n)
         if out is None:

@@ -2,7 +2,8 @@
 """A short run of one kernel family for rocprofv3 counter passes (round 3):
   aes   -> encrypt_vec(hex=True) of a 1.13 GB message (the bench's share
            envelope row: encrypt_kernel<14, 4, true>), 3 launches
-  prng  -> split_prng ChaCha20, 3-of-5, 2^24 (split_kernel<3,0,0,1>), 3 launches
+  prng  -> split_prng ChaCha20, 3-of-5, 2^24 (split_prng_kernel<3,false>), 3 launches
+  prng8 -> the same with ChaCha8 (its write floor)
   msv   -> make_shares_vec(2^24, 5) on SecretShare(3): the fused MT19937 draw +
            split (mt_jump_kernel levels, mt_gen_kernel<3>), 3 calls
 """
@@ -42,6 +43,6 @@ else:
     sec = torch.randint(-(1 << 62), 1 << 62, (n,), dtype=torch.int64, device=dev, generator=g)
     sh = torch.empty((5, field.vec_bytes(n)), dtype=torch.uint8, device=dev)
     for _ in range(3):
-        _native.split_prng(sec, bytes(range(32)), 0, 20, 0, sh, n, 3, 5)
+        _native.split_prng(sec, bytes(range(32)), 0, 8 if what == "prng8" else 20, 0, sh, n, 3, 5)
 torch.cuda.synchronize()
 print("ok", what)
