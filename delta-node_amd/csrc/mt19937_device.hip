@@ -1187,6 +1187,30 @@ const void* device_jobs(const MtHost& H, int* err) {
   return p;
 }
 
+// The call's end: DN_MT_SPIN_SYNC = 1 records an event behind the last
+// launch and polls it (the thread spins instead of blocking in the runtime:
+// a shorter wake-up for a call whose GPU work is tens of microseconds);
+// otherwise hipStreamSynchronize.  One event per thread, created once.
+#ifndef DN_MT_SPIN_SYNC
+#define DN_MT_SPIN_SYNC 0
+#endif
+hipError_t mt_wait(hipStream_t s) {
+#if DN_MT_SPIN_SYNC
+  thread_local hipEvent_t ev = nullptr;
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    ev = nullptr;
+    return hipStreamSynchronize(s);
+  }
+  hipError_t e = hipEventRecord(ev, s);
+  if (e != hipSuccess) return e;
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+  }
+  return e;
+#else
+  return hipStreamSynchronize(s);
+#endif
+}
+
 }  // namespace
 }  // namespace dn
 
@@ -1326,7 +1350,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
 #if !DN_MT_HOST_HEAD
   err = hipMemcpyAsync(head, sc, wh * 4, hipMemcpyDeviceToHost, s);  // flag .. final array
 #endif
-  const hipError_t serr = hipStreamSynchronize(s);
+  const hipError_t serr = mt_wait(s);
   if (err == hipSuccess) err = serr;
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   // DN_MT_FORCE_RETRY=1 (tuning build) takes the rejected-draw exit so the

@@ -23,5 +23,9 @@ cut -c1-400 $O/bench_n1.json
 [ $rc -ne 0 ] && { echo "== rc $rc"; tail -5 $O/bench_n1.err; exit $rc; }
 echo "== rocprof" && cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d /tmp/prof_f -o run --output-format csv -- python3 "$R/bench.py" --cpu-budget 0 > "$R/$O/bench_under_rocprof.json" 2> "$R/$O/rocprof.err" || rc=$?
 cd "$R" && mkdir -p $O/prof && find /tmp/prof_f -name "*stats.csv" -exec cp {} $O/prof/ \;
+# (appended) spin-wait call end A/B: in-tree library vs lib/ab/libdn_shamir_spinsync.so
+[ $rc -ne 0 ] && exit $rc
+TAG=r04f_ab VARIANTS=spinsync NOTEST=1 ROUNDS=2 bash scripts/ab_libs.sh > $O/ab_spinsync.log 2>&1 || rc=$?
+grep -A3 "^-- " $O/ab_spinsync.log | cut -c1-300
 echo "== rc $rc"
 exit $rc
