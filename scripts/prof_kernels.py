@@ -16,7 +16,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from delta_node.crypto import shamir  # noqa: E402
-from delta_node.crypto.shamir import _native, field  # noqa: E402
+from delta_node.crypto.shamir import _native, field, memory  # noqa: E402
 
 reps = int(os.environ.get("REPS", "5"))
 log2n = int(os.environ.get("LOG2N", "24"))
@@ -27,7 +27,7 @@ sec = torch.from_numpy(rng.integers(-(1 << 63), (1 << 63) - 1, size=N, endpoint=
 ss = shamir.SecretShare(3)
 ss.random.seed(1)
 coeffs = ss.draw_coeffs_vec(N, dev)
-shares = torch.empty((5, field.vec_bytes(N)), dtype=torch.uint8, device=dev)
+shares = memory.share_block((5, field.vec_bytes(N)), dev)  # as bench.py's blocks
 rec = torch.empty(N, dtype=torch.int64, device=dev)
 w = _native.lagrange([1, 3, 5], 3)
 torch.cuda.synchronize()
