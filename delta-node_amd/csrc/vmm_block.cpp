@@ -106,6 +106,15 @@ extern "C" int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, 
   return DN_OK;
 }
 
+// A freed block gives its physical chunks back but never its virtual range:
+// the range stays reserved (retired), so no later block or allocation is ever
+// placed at an address a freed block's translations used.  Re-reserving a
+// freed range gave a new block the old block's address, and that block's
+// contents then changed under unrelated allocations
+// (scripts/msv_block_debug.py, pass r04i: every new block at a freed block's
+// address; never otherwise).  The cost is address space only: 2^47 bytes
+// retire ~25,000 freed 5.5 GB blocks, and frees are rare (the Python pool
+// reuses idle blocks; memory.empty_cache() and pool overflow free).
 extern "C" int dn_block_free(void* ptr) {
   if (!ptr) return DN_OK;
   Block b;
@@ -116,10 +125,18 @@ extern "C" int dn_block_free(void* ptr) {
     b = std::move(it->second);
     blocks().erase(it);
   }
-  // kernels still writing the block finish before its pages go (a free is rare)
-  (void)hipDeviceSynchronize();
+  // kernels still using the block finish before its pages go (a free is rare)
+  hipError_t first = hipDeviceSynchronize();
   // per-chunk unmap: every mapping was made chunk by chunk
-  for (uint64_t off = 0; off < b.span; off += b.chunk) (void)hipMemUnmap(static_cast<uint8_t*>(ptr) + off, b.chunk);
-  release(ptr, b, 0);
+  for (uint64_t off = 0; off < b.span; off += b.chunk) {
+    const hipError_t e = hipMemUnmap(static_cast<uint8_t*>(ptr) + off, b.chunk);
+    if (first == hipSuccess) first = e;
+  }
+  for (auto h : b.handles) {
+    const hipError_t e = hipMemRelease(h);
+    if (first == hipSuccess) first = e;
+  }
+  b.handles.clear();
+  if (first != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_free: %s", hipGetErrorString(first));
   return DN_OK;
 }

@@ -79,6 +79,28 @@ def test_make_shares_vec_default_output_is_share_block():
     assert tuple(small.shape) == (5, field.vec_bytes(1000))
 
 
+def test_freed_block_address_is_never_reused():
+    """A freed block's virtual range is retired (csrc/vmm_block.cpp): the next
+    block lands elsewhere, and its bytes stay put under later allocations.
+    (Before: a new block at a freed block's address had its contents change
+    under unrelated torch allocations — scripts/msv_block_debug.py, r04i.)"""
+    memory.empty_cache()
+    shape = (5, field.vec_bytes(1 << 18))
+    seen = set()
+    for k in range(3):
+        b = memory.chunked_block(shape, device=dev(), pooled=False)
+        assert b.data_ptr() not in seen
+        seen.add(b.data_ptr())
+        b.fill_(0xA0 + k)
+        junk = [torch.full((shape[0] * shape[1],), 7, dtype=torch.uint8, device=dev()) for _ in range(3)]
+        torch.cuda.synchronize()
+        assert int((b != 0xA0 + k).sum().item()) == 0
+        del b, junk
+        gc.collect()
+    st = memory.pool_stats()
+    assert st["idle_blocks"] == 0
+
+
 def test_block_free_rejects_foreign_pointer():
     x = torch.empty(16, dtype=torch.uint8, device=dev())
     assert _native.lib().dn_block_free(x.data_ptr()) == _native.DN_ERR_ARG
