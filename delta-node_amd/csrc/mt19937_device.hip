@@ -807,13 +807,15 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
         return static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + e0 + 64u * gi));
       };
       auto bstep = [&](uint32_t gi, uint64_t cur, uint64_t& nxt) {
-        back_run<kRun>(R, M, top, lane);
+        DN_PROBE_SKIP(a, 2u) back_run<kRun>(R, M, top, lane);
         wave_sync();
         nxt = secret_of(gi ? gi - 1u : 0u);
+        DN_PROBE_SKIP(a, 1u)
         emit_split<T, SAUX, NS, true>(a, R + (gi & 1u) * group, qb + 64u * gi, lane, cur);
         wave_sync();
       };
       uint64_t secA = secret_of(ngroups - 1u), secB = secret_of(ngroups - 2u);
+      DN_PROBE_SKIP(a, 1u)
       emit_split<T, SAUX, NS, true>(a, R + group, qb + 64u * (ngroups - 1u), lane, secA);
       wave_sync();
       for (uint32_t gi = ngroups - 2u;; gi -= 2u) {
