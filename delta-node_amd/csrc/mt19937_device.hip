@@ -889,6 +889,156 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   }
 }
 
+// The fused draw + split with generation and emission on separate waves: a
+// 128-thread workgroup per substream, wave 1 (producer) appends group i + 1
+// to the LDS ring while wave 0 (consumer) emits group i (temper, split, the
+// share stores), one workgroup barrier per group.  A group's words depend on
+// the 624 words before it only (a group is 2176 words or more), so the
+// producer writes the ring half the consumer emitted one step earlier while
+// both read the other: the emission (at the share block's write rate) no
+// longer waits for the generation, which in mt_gen_kernel's one wave per
+// substream runs between two emissions (r04i: full 1.02 ms, emission alone
+// 0.93, generation alone 0.50 at 2^24 3-of-5 on a share block).  Backward
+// substreams the same way downwards.  Same output and final state as
+// mt_gen_kernel<T> (T = 2, 3, 5; the coefficient draw keeps one wave).
+// Dynamic LDS as mt_gen_kernel; registers for 4 waves per SIMD (8 workgroups
+// per CU, the most the rings' LDS allows at t <= 3), 2 at t = 5 (4 fit).
+template <int T, int SAUX = kNt, int NS = 0>
+__global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const GenArgs a) {
+  static_assert(T >= 2, "fused split only");
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+  const uint32_t lane = threadIdx.x & 63u;
+  // (roles alternating with the workgroup's parity: no faster, profiles/r04/l/)
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 consumer, 1 producer
+  const uint32_t sub = blockIdx.x;
+  if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
+  const bool fin_wave = sub == a.S;
+  const bool fwd = fin_wave || mt_sub_forward(sub, a.S, static_cast<int>(a.back));
+  const uint32_t sub_words = 17u * static_cast<uint32_t>(a.sub_draws);
+  const uint32_t wsel = fin_wave ? static_cast<uint32_t>(a.final_sig) : fwd ? sub : sub + 1u;
+  const uint32_t* win = a.wins + static_cast<uint64_t>(wsel) * kMtN;
+  const uint32_t p_start = (sub == 0 && !fin_wave) ? kMtN - a.idx : fwd ? 0u : sub_words;
+  GenRing g;
+  g.M = a.ring;
+  g.delta = (64u - (p_start & 63u)) & 63u;
+  g.o = g.delta & 1u;
+  uint32_t* R = s_ring;
+  uint32_t slot = __builtin_amdgcn_readfirstlane((p_start + g.delta) % g.M);  // producer: slot of the next append
+  if (fin_wave) {
+    if (wid != 0u) return;  // one wave steps to CPython's final array (as mt_gen_kernel)
+    ring_init(R, g, win, p_start, lane);
+    wave_sync();
+    const uint64_t P = a.final_pos, tf = a.final_tf;
+    for (uint32_t i = lane; i < static_cast<uint32_t>(kMtN); i += 64u)
+      if (P + i >= tf && P + i < tf + kMtN) a.fin[P + i - tf] = win[i];
+    uint64_t np = P + kMtN;
+    while (np < tf + kMtN) {
+      uint32_t v[3];
+      ring_batch<3>(R, g, slot, lane, v);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint64_t x = np + 64u * k + lane;
+        if (x >= tf && x < tf + kMtN) a.fin[x - tf] = v[k];
+      }
+      np += 192u;
+    }
+    return;
+  }
+  const uint32_t group = a.ring / 2u;
+  const uint64_t k0 = static_cast<uint64_t>(sub) * a.sub_draws;
+  const uint32_t nloc = static_cast<uint32_t>(a.ncoef - k0 < a.sub_draws ? a.ncoef - k0 : a.sub_draws);
+  constexpr uint32_t gdraws = 64u * (T - 1);
+  const uint32_t ngroups = (nloc + gdraws - 1u) / gdraws;
+  const uint64_t qb = k0 / static_cast<uint64_t>(a.tm1);
+  constexpr int kRun = 17 * (T - 1);
+  static_assert(kRun > 10, "a group holds the 640 words under the window");
+  const bool prod = wid == 1u;
+  if (!fwd) {
+    // backward (whole groups, ngroups even; group gi in ring half gi % 2):
+    // the producer fills the top group under the window, then per step
+    // generates group gi - 1 while the consumer emits group gi
+    const uint32_t M = a.ring;
+    uint32_t top = M - 640u;
+    if (prod) {
+      ring_init(R, g, win, p_start, lane);
+      wave_sync();
+      back_blocks<1, true, true>(R, M, M - 576u, lane, M - 624u);
+      back_run<kRun - 10>(R, M, top, lane);
+    }
+    __syncthreads();
+    const uint64_t e0 = qb + lane;
+    auto secret_of = [&](uint32_t gi) {
+      return static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + e0 + 64u * gi));
+    };
+    uint64_t secA = 0, secB = 0;
+    if (!prod) secA = secret_of(ngroups - 1u);
+    // step j emits group gi = ngroups - 1 - j (secret in cur, the next one's
+    // loaded into nxt before the stores) and generates group gi - 1
+    auto bstep = [&](uint32_t gi, uint64_t cur, uint64_t& nxt) {
+      if (prod) {
+        if (gi > 0u) {
+          DN_PROBE_SKIP(a, 2u) back_run<kRun>(R, M, top, lane);
+        }
+      } else {
+        nxt = secret_of(gi ? gi - 1u : 0u);
+        DN_PROBE_SKIP(a, 1u)
+        emit_split<T, SAUX, NS, true>(a, R + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+      }
+      __syncthreads();
+    };
+    for (uint32_t gi = ngroups - 1u;; gi -= 2u) {
+      bstep(gi, secA, secB);
+      bstep(gi - 1u, secB, secA);
+      if (gi == 1u) break;
+    }
+    if (!prod) asm volatile("" : : "v"(secA ^ secB));  // no load left in flight at the end
+    return;
+  }
+  // forward: step i generates group i (producer) and emits group i - 1 (consumer)
+  if (prod) {
+    ring_init(R, g, win, p_start, lane);
+    wave_sync();
+  }
+  const uint64_t e0 = qb + lane;
+  const uint64_t elast = a.n_elem - 1u;
+  auto secret_of = [&](uint32_t gi) {
+    const uint64_t e = e0 + 64u * gi;
+    return static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + (e < elast ? e : elast)));
+  };
+  const uint64_t rem = a.n_elem - qb;
+  const uint32_t nfull = rem >= 64ull * ngroups ? ngroups : static_cast<uint32_t>(rem / 64u);
+  // the consumer's secrets: group i - 1's in cur, group i's loaded into nxt
+  // before the stores (two registers by parity, as mt_gen_kernel)
+  auto fstep = [&](uint32_t i, uint64_t cur, uint64_t& nxt) {
+    if (prod) {
+      if (i < ngroups) {
+        DN_PROBE_SKIP(a, 2u) ring_run<kRun>(R, g, slot, lane);
+      }
+    } else if (i >= 1u) {
+      const uint32_t gi = i - 1u;
+      nxt = secret_of(i);
+      if (gi < nfull) {
+        DN_PROBE_SKIP(a, 1u)
+        emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+      } else {  // the vector's last, partial group
+        emit_split<T, SAUX, NS, false>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+      }
+    }
+    __syncthreads();
+  };
+  uint64_t secA = 0, secB = 0;
+  if (!prod) secA = secret_of(0);
+  fstep(0u, 0u, secB);  // group 0 generated; nothing to emit (secB untouched)
+  uint32_t i = 1u;
+  for (; i + 1u <= ngroups; i += 2u) {
+    fstep(i, secA, secB);
+    if (i + 1u > ngroups) break;
+    fstep(i + 1u, secB, secA);
+  }
+  if (i <= ngroups) fstep(i, secA, secB);
+  if (!prod) asm volatile("" : : "v"(secA ^ secB));
+}
+
 uint64_t mt_subs(uint64_t ncoef) {
   const uint64_t d = mt_sub_draws(mt_sub_len(ncoef));
   return (ncoef + d - 1) / d;
@@ -1367,7 +1517,12 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
 #ifndef DN_MT_SAUX
 #define DN_MT_SAUX 16
 #endif
-constexpr int kSc1 = DN_MT_SAUX;  // buffer-store cache policy of the 3-of-5 share stores: sc1 (16)
+constexpr int kSc1 = DN_MT_SAUX;
+// the fused split's generation and emission on two waves per substream for
+// draws of few substreams (mt_gen_pc_kernel; 0: always one wave, mt_gen_kernel)
+#ifndef DN_MT_PC
+#define DN_MT_PC 1
+#endif  // buffer-store cache policy of the 3-of-5 share stores: sc1 (16)
 
 template <int T>
 void launch_gen(GenArgs& ga, hipStream_t s) {
@@ -1391,6 +1546,21 @@ void launch_gen(GenArgs& ga, hipStream_t s) {
   // the headline 3-of-5: straight-line share stores (see mt_gen_kernel), sc1
   // rather than non-temporal: 2.2 % faster on two buffers of one process
   // (profiles/r03/ab/mt_store_aux_ns5.json)
+  // Two waves per substream pay off while the one-wave kernel would hold at
+  // most one wave per SIMD (S + 1 <= 4 per CU): make_shares_vec 2^20 / 2^16 /
+  // 2^12 -12 / -8 / -3 %; with every CU's 8 ring slots taken (2^24: S + 1 =
+  // 2049) both are bound by the share writes and the one-wave kernel was 9 %
+  // faster (profiles/r04/l/).
+  if constexpr (T >= 2 && DN_MT_PC) {
+    if (static_cast<uint64_t>(ga.S) + 1u <= 4u * static_cast<uint64_t>(device_cu_count())) {
+      if (T == 3 && ga.n_shares == 5)
+        hipLaunchKernelGGL((mt_gen_pc_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(128), lds_words * 4u, s,
+                           ga);
+      else
+        hipLaunchKernelGGL((mt_gen_pc_kernel<T>), dim3(ga.S + 1), dim3(128), lds_words * 4u, s, ga);
+      return;
+    }
+  }
   if (T == 3 && ga.n_shares == 5)
     hipLaunchKernelGGL((mt_gen_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
   else
