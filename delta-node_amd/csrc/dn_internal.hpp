@@ -47,4 +47,13 @@ uint64_t mt_jump_words();
 uint64_t mt_jump_max_subs();
 void mt_advance_window(const uint32_t* win, uint64_t steps, uint32_t* out);
 bool mt_final_state(const uint32_t* state, int idx, uint64_t words, uint32_t* fin, int32_t* fidx);
+
+// Runtime direct jump rows (host_gf2poly.cpp): D_s = x^(L - 624 + (s - 1) L)
+// mod P, L = 17 * 2^14 words, row s - 1 of kMtPolyWords uint64, for the
+// windows a backward-generating draw of S <= kMtRtRows + 1 substreams needs
+// (odd s < S and S - 1); computed on first use and cached; *version changes
+// whenever rows were added (nullptr: no carry-less multiply on this host, or
+// a row disagreed with the tabulated ones).
+constexpr uint64_t kMtRtRows = 2048;
+const uint64_t* mt_direct_rows_l14(uint64_t S, uint64_t* version);
 }  // namespace dn

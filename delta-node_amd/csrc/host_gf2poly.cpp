@@ -1,0 +1,160 @@
+// host_gf2poly.cpp — MT19937 jump polynomials computed on the host at run time
+// (plain C++; mt19937_device.hip uses them).
+//
+// The device draw reaches substream window s by jumps g(f) W with
+// g = x^J mod P (P the characteristic polynomial of the one-word transition,
+// degree 19937; tools/gen_mt_jump.py).  For the largest draws it can take one
+// direct level instead of the radix-64 levels A then B if it has
+// D_s = x^(L - 624 + (s - 1) L) mod P for s up to ~2048 (L = 17 * 2^14): too
+// many rows to tabulate in source (5 MB), so they are computed here once per
+// process as D_{s+1} = D_s * x^L mod P from the tabulated D_1 and x^L = B_1,
+// one GF(2)[x] product and one Barrett reduction per row (carry-less
+// multiplies), and checked against the 63 tabulated direct rows D_2..D_64.
+#include <immintrin.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "dn_internal.hpp"
+
+namespace dn {
+namespace {
+
+#include "mt19937_charpoly.inc"
+#include "mt19937_jump.inc"
+#include "mt19937_jump_direct.inc"
+
+constexpr int kW = kMtPolyWords;  // 312 words: degree < 19937
+constexpr int kDeg = 19937;
+static_assert(kW * 64 > kDeg && (kW - 1) * 64 <= kDeg, "poly words");
+
+const uint64_t kP[1][kW] = DN_MT_CHAR_POLY;
+const uint64_t kJump14[kMtJumpRows][kW] = DN_MT_JUMP_POLYS;
+const uint64_t kDirect14[kMtDirectRows][kW] = DN_MT_JUMP_DIRECT_L14;
+
+// r[0 .. na + nb) = a * b (carry-less), column by column: the 128-bit
+// products of word pairs (i, k - i) XOR into one register, two output words
+// per column, so the inner loop has no memory traffic
+__attribute__((target("pclmul,sse4.1"))) void clmul_poly(const uint64_t* a, int na, const uint64_t* b, int nb,
+                                                          uint64_t* r) {
+  std::memset(r, 0, sizeof(uint64_t) * (na + nb));
+  for (int k = 0; k < na + nb - 1; ++k) {
+    const int i0 = k - nb + 1 > 0 ? k - nb + 1 : 0, i1 = k < na - 1 ? k : na - 1;
+    __m128i acc = _mm_setzero_si128(), acc2 = _mm_setzero_si128();
+    int i = i0;
+    for (; i + 1 <= i1; i += 2) {  // two independent chains; b[k - i - 1], b[k - i] as one load
+      const __m128i av = _mm_loadu_si128(reinterpret_cast<const __m128i*>(a + i));
+      const __m128i bv = _mm_loadu_si128(reinterpret_cast<const __m128i*>(b + k - i - 1));
+      acc = _mm_xor_si128(acc, _mm_clmulepi64_si128(av, bv, 0x10));   // a[i] * b[k - i]
+      acc2 = _mm_xor_si128(acc2, _mm_clmulepi64_si128(av, bv, 0x01));  // a[i + 1] * b[k - i - 1]
+    }
+    if (i <= i1)
+      acc = _mm_xor_si128(acc, _mm_clmulepi64_si128(_mm_loadl_epi64(reinterpret_cast<const __m128i*>(a + i)),
+                                                     _mm_loadl_epi64(reinterpret_cast<const __m128i*>(b + k - i)), 0x00));
+    acc = _mm_xor_si128(acc, acc2);
+    r[k] ^= static_cast<uint64_t>(_mm_cvtsi128_si64(acc));
+    r[k + 1] ^= static_cast<uint64_t>(_mm_extract_epi64(acc, 1));
+  }
+}
+
+// out[0 .. n) = words of (a >> sh bits), a of na words
+void shr_bits(const uint64_t* a, int na, int sh, uint64_t* out, int n) {
+  const int ws = sh / 64, bs = sh % 64;
+  for (int i = 0; i < n; ++i) {
+    const int k = i + ws;
+    const uint64_t lo = k < na ? a[k] : 0u;
+    const uint64_t hi = k + 1 < na ? a[k + 1] : 0u;
+    out[i] = bs ? (lo >> bs) | (hi << (64 - bs)) : lo;
+  }
+}
+
+bool bit(const uint64_t* a, int i) { return (a[i / 64] >> (i % 64)) & 1u; }
+
+struct Barrett {
+  std::vector<uint64_t> mu;  // floor(x^(2 deg) / P): degree deg, kW words
+  Barrett() : mu(kW, 0) {
+    // long division of x^(2 deg) by P, one quotient bit at a time
+    std::vector<uint64_t> r(2 * kW + 1, 0);
+    r[(2 * kDeg) / 64] |= 1ull << ((2 * kDeg) % 64);
+    for (int i = 2 * kDeg; i >= kDeg; --i) {
+      if (!bit(r.data(), i)) continue;
+      mu[(i - kDeg) / 64] |= 1ull << ((i - kDeg) % 64);
+      const int sh = i - kDeg, ws = sh / 64, bs = sh % 64;  // r ^= P << sh
+      for (int k = 0; k < kW; ++k) {
+        const uint64_t w = kP[0][k];
+        r[k + ws] ^= w << bs;
+        if (bs) r[k + ws + 1] ^= w >> (64 - bs);
+      }
+    }
+  }
+  // out = a * b mod P (a, b of degree < deg)
+  void mulmod(const uint64_t* a, const uint64_t* b, uint64_t* out) const {
+    std::vector<uint64_t> c(2 * kW), hi(kW), t(2 * kW), q(kW), qp(2 * kW);
+    clmul_poly(a, kW, b, kW, c.data());
+    shr_bits(c.data(), 2 * kW, kDeg, hi.data(), kW);  // c / x^deg
+    clmul_poly(hi.data(), kW, mu.data(), kW, t.data());
+    shr_bits(t.data(), 2 * kW, kDeg, q.data(), kW);  // quotient
+    clmul_poly(q.data(), kW, kP[0], kW, qp.data());
+    for (int k = 0; k < kW; ++k) out[k] = c[k] ^ qp[k];
+    out[kW - 1] &= (1ull << (kDeg % 64)) - 1u;  // bits >= deg are zero in c ^ qP
+  }
+};
+
+struct Rows {
+  std::mutex m;
+  std::vector<uint64_t> rows;  // row s - 1 = D_s; allocated once (pointers stay valid)
+  std::vector<uint8_t> have;   // row computed
+  uint64_t odd_top = 0;        // D_1, D_3, .., D_odd_top computed in sequence
+  uint64_t version = 0;        // rows computed so far (changes when any row is added)
+  bool ok = true;
+  Barrett* br = nullptr;
+};
+
+Rows& rows14() {
+  static Rows* r = new Rows;  // never destroyed
+  return *r;
+}
+
+bool set_row(Rows& R, uint64_t s, const uint64_t* prev, const uint64_t* mul) {
+  uint64_t* out = R.rows.data() + (s - 1) * kW;
+  R.br->mulmod(prev, mul, out);
+  R.have[s - 1] = 1;
+  ++R.version;
+  // the tabulated direct rows D_2 .. D_64 check the arithmetic
+  if (s <= static_cast<uint64_t>(kMtDirectRows) && std::memcmp(out, kDirect14[s - 1], sizeof(uint64_t) * kW)) {
+    R.ok = false;
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+const uint64_t* mt_direct_rows_l14(uint64_t S, uint64_t* version) {
+  if (S < 2 || S - 1 > kMtRtRows || !__builtin_cpu_supports("pclmul")) return nullptr;
+  Rows& R = rows14();
+  std::lock_guard<std::mutex> g(R.m);
+  if (!R.ok) return nullptr;
+  if (R.rows.empty()) {
+    R.rows.assign(static_cast<size_t>(kMtRtRows) * kW, 0u);
+    R.have.assign(kMtRtRows, 0u);
+    R.br = new Barrett;
+    std::memcpy(R.rows.data(), kDirect14[0], sizeof(uint64_t) * kW);  // D_1
+    R.have[0] = 1;
+    R.odd_top = 1;
+    if (!set_row(R, 2, R.rows.data(), kJump14[kMtRowB + 1])) return nullptr;  // D_2 = D_1 x^L, checked
+  }
+  // the windows a backward-generating draw of S substreams starts from: odd
+  // s < S (D_{s+2} = D_s x^(2L), B_2 = x^(2L)) and the last, S - 1
+  const uint64_t last = S - 1;
+  for (uint64_t s = R.odd_top + 2; s <= last; s += 2, R.odd_top += 2)
+    if (!set_row(R, s, R.rows.data() + (s - 3) * kW, kJump14[kMtRowB + 2])) return nullptr;
+  if (!R.have[last - 1] && !set_row(R, last, R.rows.data() + (last - 2) * kW, kJump14[kMtRowB + 1]))
+    return nullptr;
+  if (version) *version = R.version;
+  return R.rows.data();
+}
+
+}  // namespace dn

@@ -71,6 +71,9 @@ __device__ const uint64_t kMtDirectDev[kMtLens][kMtDirectRows][kMtPolyWords] = {
     DN_MT_JUMP_DIRECT_L10, DN_MT_JUMP_DIRECT_L12, DN_MT_JUMP_DIRECT_L14, DN_MT_JUMP_DIRECT_L8};
 static_assert(kMtJumpL8 == 17ull << 8, "table lengths");
 constexpr int32_t kMtDirectBase = kMtTabLens * kMtJumpRows;
+// Runtime direct rows (host_gf2poly.cpp, kMtRtRows of them for L = 17 * 2^14,
+// uploaded once per device): job poly indices from kMtRtBase address them.
+constexpr int32_t kMtRtBase = kMtDirectBase + kMtLens * kMtDirectRows;
 
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -122,6 +125,12 @@ struct JumpJob {
   int32_t span;            // words [lo, hi) of g this job evaluates: lo | hi << 16
 };
 
+// The runtime direct level (build_levels' rt; DN_MT_RT=0 in the tuning
+// build turns it off for A/B).
+#ifndef DN_MT_RT_DIRECT
+#define DN_MT_RT_DIRECT 1
+#endif
+
 // A latency-bound level (few jobs: one Horner chain of ~312 steps per jump)
 // splits every jump into P parts over word ranges [lo, hi) of g.  Since
 // g(f) W = sum_k f^(64 k) g_k(f) W, part [lo, hi) evaluates
@@ -137,6 +146,7 @@ struct JumpArgs {
   const JumpJob* jobs;
   uint32_t njobs;
   uint32_t probe;  // tuning build only (DN_MT_JUMP_PROBE): 1 = no Horner steps, 2 = no stream stepping (timing only)
+  const uint64_t* rt;  // runtime direct rows on the device (poly >= kMtRtBase), or null
 };
 
 // Jump and generation waves keep a 624-word MT window in registers: Q[11] a
@@ -341,10 +351,12 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   __syncthreads();
   if (j0 + wid >= a.njobs || dsti < 0) return;
 
-  // poly = table * rows + row, or kMtDirectBase + length * 64 + s - 1 (wave-uniform)
-  const uint64_t* g = poly < kMtDirectBase
-                          ? &kMtPolysDev[0][0][0] + static_cast<uint64_t>(poly) * kMtPolyWords
-                          : &kMtDirectDev[0][0][0] + static_cast<uint64_t>(poly - kMtDirectBase) * kMtPolyWords;
+  // poly = table * rows + row, kMtDirectBase + length * 64 + s - 1, or
+  // kMtRtBase + s - 1 (wave-uniform)
+  const uint64_t* g = poly < kMtDirectBase ? &kMtPolysDev[0][0][0] + static_cast<uint64_t>(poly) * kMtPolyWords
+                      : poly < kMtRtBase
+                          ? &kMtDirectDev[0][0][0] + static_cast<uint64_t>(poly - kMtDirectBase) * kMtPolyWords
+                          : a.rt + static_cast<uint64_t>(poly - kMtRtBase) * kMtPolyWords;
   uint32_t Q[11];
 #pragma unroll
   for (int r = 0; r < 11; ++r) Q[r] = 0u;
@@ -1145,11 +1157,23 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
 // A: W(1 + 64 a) = A_a(W_idx); C: W(1 + 4096 c + 64 a) = C_c(W(1 + 64 a));
 // B: W(base + b) = B_b(W(base)).  back: only the windows a generation wave
 // starts from (mt_sub_forward: odd s, the last one) — A and C windows are odd.
-void build_levels(uint64_t S, int ki, int back, Level lv[3]) {
+// rt: one direct level through the runtime rows (host_gf2poly.cpp) for the
+// draws of up to kMtRtRows + 1 substreams of 2^14 draws that generate
+// backward: the 1024 windows of a 2^24-element 3-of-5 draw in one level of
+// ~150 us instead of level A (~28 us), its combine and level B (~148 us).
+void build_levels(uint64_t S, int ki, int back, bool rt, Level lv[3]) {
   const uint64_t R = kMtJumpRadix;
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
   const int32_t prow0 = static_cast<int32_t>(S + 1);
+  if (rt) {
+    std::vector<std::pair<int32_t, int32_t>> pd;
+    for (uint64_t s = 1; s < S; ++s)
+      if (mt_window_needed(static_cast<uint32_t>(s), S, back))
+        pd.push_back({kMtRtBase + static_cast<int32_t>(s - 1), static_cast<int32_t>(s)});
+    push_level(lv[0], {{-1, pd}}, prow0);
+    return;
+  }
   if (last < static_cast<uint64_t>(kMtDirectRows)) {
     // every window one jump from W_idx: W(s) = D_s(W_idx), one level
     std::vector<std::pair<int32_t, int32_t>> pd;
@@ -1197,6 +1221,7 @@ struct MtHost {
   int ki = -1;
   int back = 0;
   int parts_b = 0;  // tuning build: DN_MT_PARTS_B the levels were built with
+  bool rt = false;  // one direct level through the runtime rows
   Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
@@ -1218,9 +1243,16 @@ MtHost& mt_levels(uint64_t S, int ki) {
   const int back = ki == 3 ? 0 : mt_back();
   const char* pb = tune_env("DN_MT_PARTS_B");
   const int parts_b = pb ? std::atoi(pb) : 0;
-  if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b) {
+  // the runtime direct level: 2^14-draw substreams generating backward, more
+  // than the tabulated direct rows cover, at most kMtRtRows + 1 of them, and
+  // rows available on this host (DN_MT_RT=0, tuning build: off)
+  const char* rte = tune_env("DN_MT_RT");
+  const bool rt = DN_MT_RT_DIRECT && !(rte && rte[0] == '0') && ki == 2 && back == 1 &&
+                  S - 1 > static_cast<uint64_t>(kMtDirectRows) && S - 1 <= kMtRtRows &&
+                  mt_direct_rows_l14(S, nullptr) != nullptr;
+  if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b || H.rt != rt) {
     for (auto& l : H.lv) l = Level();
-    build_levels(S, ki, back, H.lv);
+    build_levels(S, ki, back, rt, H.lv);
     uint64_t nj = 0, nc = 0;
     for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
     H.part_rows = 0;
@@ -1240,6 +1272,7 @@ MtHost& mt_levels(uint64_t S, int ki) {
     H.ki = ki;
     H.back = back;
     H.parts_b = parts_b;
+    H.rt = rt;
   }
   return H;
 }
@@ -1313,6 +1346,7 @@ struct DevJobs {
   int dev;
   uint64_t S;
   int ki, back, parts_b;
+  bool rt;
   void* p;
 };
 
@@ -1326,7 +1360,8 @@ const void* device_jobs(const MtHost& H, int* err) {
   }
   std::lock_guard<std::mutex> g(*m);
   for (const DevJobs& d : *cache)
-    if (d.dev == dev && d.S == H.S && d.ki == H.ki && d.back == H.back && d.parts_b == H.parts_b) return d.p;
+    if (d.dev == dev && d.S == H.S && d.ki == H.ki && d.back == H.back && d.parts_b == H.parts_b && d.rt == H.rt)
+      return d.p;
   void* p = nullptr;
   const size_t bytes = std::max<size_t>(H.jobs.size() * 4, 16);
   if (hipMalloc(&p, bytes) != hipSuccess ||
@@ -1335,8 +1370,53 @@ const void* device_jobs(const MtHost& H, int* err) {
     *err = 1;
     return nullptr;
   }
-  cache->push_back({dev, H.S, H.ki, H.back, H.parts_b, p});
+  cache->push_back({dev, H.S, H.ki, H.back, H.parts_b, H.rt, p});
   return p;
+}
+
+// The runtime direct rows on the device: one kMtRtRows-row buffer per device,
+// rows copied when the host has computed rows the device copy lacks (rows are
+// only ever added, never changed).  Library-owned, never freed (5.1 MB).
+struct DevRt {
+  int dev;
+  uint64_t* p;
+  uint64_t version, rows;
+};
+
+const uint64_t* device_rt(uint64_t S, int* err) {
+  static std::mutex* m = new std::mutex;
+  static auto* cache = new std::vector<DevRt>;
+  uint64_t version = 0;
+  const uint64_t* host = mt_direct_rows_l14(S, &version);
+  int dev = 0;
+  if (!host || hipGetDevice(&dev) != hipSuccess) {
+    *err = 1;
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(*m);
+  DevRt* d = nullptr;
+  for (DevRt& c : *cache)
+    if (c.dev == dev) d = &c;
+  if (!d) {
+    void* p = nullptr;
+    if (hipMalloc(&p, kMtRtRows * kMtPolyWords * sizeof(uint64_t)) != hipSuccess) {
+      *err = 1;
+      return nullptr;
+    }
+    cache->push_back({dev, static_cast<uint64_t*>(p), 0, 0});
+    d = &cache->back();
+  }
+  const uint64_t need = S - 1;
+  if (d->version != version || d->rows < need) {
+    const uint64_t n = std::max(d->rows, need);
+    if (hipMemcpy(d->p, host, n * kMtPolyWords * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) {
+      *err = 1;
+      return nullptr;
+    }
+    d->version = version;
+    d->rows = n;
+  }
+  return d->p;
 }
 
 // The call's end: DN_MT_SPIN_SYNC = 1 records an event behind the last
@@ -1428,6 +1508,8 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   int jerr = 0;
   const void* jobs_dev = device_jobs(H, &jerr);
   if (jerr) return set_error(DN_ERR_HIP, "%s: job tables on the device", name);
+  const uint64_t* rt_dev = H.rt ? device_rt(S, &jerr) : nullptr;
+  if (jerr) return set_error(DN_ERR_HIP, "%s: runtime jump rows on the device", name);
   const size_t wpre = kHead / 4 + 2 * kMtN, wh = 256 / 4 + kMtN;
   PinLease lease(wpre + wh);  // idle again once this call has synchronised its stream
   uint32_t* pin = lease.p;
@@ -1452,7 +1534,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     if (!l.jobs.empty()) {
       const char* jpr = tune_env("DN_MT_JUMP_PROBE");
       const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.jobs.size()),
-                        jpr ? static_cast<uint32_t>(std::atoi(jpr)) : 0u};
+                        jpr ? static_cast<uint32_t>(std::atoi(jpr)) : 0u, rt_dev};
       const dim3 grid(static_cast<uint32_t>(l.jobs.size() / static_cast<size_t>(l.W)));
       if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, s, ja);
       else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, s, ja);

@@ -276,10 +276,29 @@ def main_direct(out_path):
     print("wrote", out_path)
 
 
+def main_charpoly(out_path):
+    """P itself (degree 19937, 312 words): the device draw's host side
+    multiplies tabulated rows mod P at run time (runtime direct rows,
+    mt19937_device.hip)."""
+    P = char_poly()
+    nw = (DEG + 1 + 63) // 64
+    assert P.bit_length() - 1 == DEG
+    # x^L mod P from P agrees with the tabulated B_1 for L = 17 * 2^14
+    assert xpow(L_WORDS, P) == jump_polys(P, L_WORDS)[2 * RADIX - 1][2]
+    with open(out_path, "w") as f:
+        f.write("// Generated by tools/gen_mt_jump.py --charpoly — do not edit.\n")
+        f.write("// P, the characteristic polynomial of MT19937's one-word transition\n")
+        f.write("// (degree 19937; bit i of word i/64 is the coefficient of x^i).\n")
+        write_polys(f, "DN_MT_CHAR_POLY", [("P", 0, P)])
+    print("wrote", out_path)
+
+
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     csrc = os.path.join(root, "delta-node_amd", "csrc")
-    if len(sys.argv) > 1 and sys.argv[1] == "--direct":
+    if len(sys.argv) > 1 and sys.argv[1] == "--charpoly":
+        main_charpoly(sys.argv[2] if len(sys.argv) > 2 else os.path.join(csrc, "mt19937_charpoly.inc"))
+    elif len(sys.argv) > 1 and sys.argv[1] == "--direct":
         main_direct(sys.argv[2] if len(sys.argv) > 2 else os.path.join(csrc, "mt19937_jump_direct.inc"))
     elif len(sys.argv) > 1 and sys.argv[1] == "--short":
         main_short(sys.argv[2] if len(sys.argv) > 2 else os.path.join(csrc, "mt19937_jump_short.inc"))

@@ -17,13 +17,17 @@
 #include <set>
 namespace dn { int set_error(int c, const char*, ...) { return c; } int device_cu_count() { return 256; }
 uint64_t mt_jump_words() { return 0; } uint64_t mt_jump_max_subs() { return 262145; }
-void mt_advance_window(const uint32_t*, uint64_t, uint32_t*) {} }
+void mt_advance_window(const uint32_t*, uint64_t, uint32_t*) {}
+const uint64_t* mt_direct_rows_l14(uint64_t, uint64_t*) { return nullptr; } }
 using namespace dn;
 extern "C" uint64_t dn_m521_vec_bytes(uint64_t n) { return n; }
-int check(uint64_t S, int ki, int back) {
-  const bool direct = S - 1 <= static_cast<uint64_t>(kMtDirectRows);
+int check(uint64_t S, int ki, int back, bool rt = false) {
+  const bool direct = S - 1 <= static_cast<uint64_t>(kMtDirectRows) || rt;
+  // direct rows of this level: the tabulated D_s of length ki, or the runtime rows
+  const int32_t dbase = rt ? kMtRtBase : kMtDirectBase + ki * kMtDirectRows;
+  const int32_t dend = rt ? kMtRtBase + static_cast<int32_t>(kMtRtRows) : dbase + kMtDirectRows;
   Level LV[3];
-  build_levels(S, ki, back, LV);
+  build_levels(S, ki, back, rt, LV);
   std::vector<const Level*> lv = {&LV[0], &LV[1], &LV[2]};
   std::vector<int> known(S + 1 + kPartRows + 8, 0);
   known[0] = 1;  // the caller's array; W_idx (level A's source) is window -1
@@ -42,10 +46,8 @@ int check(uint64_t S, int ki, int back) {
         if (j.src >= 0 && !known[j.src]) { printf("S=%llu lvl %d src %d unknown\n", (unsigned long long)S, k, j.src); return 1; }
         const int lo = j.span & 0xffff, hi = j.span >> 16;
         if (direct) {  // one level from W_idx, rows D_s of this length
-          if (k != 0 || j.src != -1 || j.poly < kMtDirectBase + ki * kMtDirectRows ||
-              j.poly >= kMtDirectBase + (ki + 1) * kMtDirectRows)
-            bad++;
-          if (L.comb.empty() && j.poly != kMtDirectBase + ki * kMtDirectRows + j.dst - 1) bad++;  // W(s) <- D_s
+          if (k != 0 || j.src != -1 || j.poly < dbase || j.poly >= dend) bad++;
+          if (L.comb.empty() && j.poly != dbase + j.dst - 1) bad++;  // W(s) <- D_s
         } else if (ki >= kMtTabLens || j.poly < ki * kMtJumpRows || j.poly >= (ki + 1) * kMtJumpRows) {
           bad++;
         }
@@ -72,7 +74,7 @@ int check(uint64_t S, int ki, int back) {
         partw.erase(it);
       }
       if (expect_lo != kMtPolyWords) bad++;
-      if (direct && poly != kMtDirectBase + ki * kMtDirectRows + c.dst - 1) bad++;  // W(s) <- D_s
+      if (direct && poly != dbase + c.dst - 1) bad++;  // W(s) <- D_s
       known[c.dst] = 2;
     }
     if (!partw.empty()) bad++;
@@ -94,9 +96,12 @@ int main() {
       if (ki >= kMtTabLens && S - 1 > static_cast<uint64_t>(kMtDirectRows)) continue;  // direct-only length
       fails += check(S, ki, 0) + check(S, ki, 1);
     }
+  // the runtime direct level (2^14-draw substreams, backward generation, 65 < S <= 2049)
+  for (uint64_t S : Ss)
+    if (S - 1 > static_cast<uint64_t>(kMtDirectRows) && S - 1 <= kMtRtRows) fails += check(S, 2, 1, true);
   // summary for a few sizes
   for (uint64_t S : {2ull, 129ull, 513ull, 2049ull, 4097ull, 16385ull}) {
-    Level L[3]; build_levels(S, 2, 1, L);
+    Level L[3]; build_levels(S, 2, 1, false, L);
     printf("S=%6llu", (unsigned long long)S);
     for (int k = 0; k < 3; ++k) printf("  level %c: W=%d workgroups=%zu combines=%zu", "ACB"[k], L[k].W, L[k].jobs.size() / L[k].W, L[k].comb.size());
     printf("\n");
