@@ -239,8 +239,12 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
         coeffs = cb[:, :vb].contiguous() if cb.shape[1] != vb else cb
     else:
         coeffs = ss.draw_coeffs_vec(N_total, dev)
-    block = torch.zeros((n, B), dtype=torch.uint8, device=dev)
-    shares = block if vb == B else torch.empty((n, vb), dtype=torch.uint8, device=dev)
+    # the split writes into a share block as make_shares_vec returns one
+    # (memory.share_block); the all-gather's padded send block is separate
+    from delta_node.crypto.shamir import memory as _memory
+
+    shares = _memory.share_block((n, vb), dev)
+    block = torch.zeros((n, B), dtype=torch.uint8, device=dev) if dist_on else None
     stream = torch.cuda.current_stream()
     for _ in range(2):
         _native.split_u64(sec, coeffs, shares, nl, t, n)
@@ -251,7 +255,7 @@ def config4_bench(dev, world: int, rank: int, log2n_total: int = 26, reps: int =
         b.record(stream)
     torch.cuda.synchronize()
     split_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if shares is not block:
+    if block is not None:
         block[:, :vb].copy_(shares)
     xs = [1, 3, 5, 7, 9]
     rec = torch.empty(nl, dtype=torch.int64, device=dev)
@@ -1083,7 +1087,10 @@ def main():
                      "split_ms": split_by_buf, "frac": fr, "frac_min": min(fr), "frac_median": float(np.median(fr)),
                      "frac_max": max(fr), "n_frac_ge_0_70": sum(f >= 0.70 for f in fr),
                      "ceiling_ms": [c["ms"] for c in ceils],
-                     "split_frac_of_ceiling": [c["ms"] / ms for c, ms in zip(ceils, split_by_buf)]}
+                     "split_frac_of_ceiling": [c["ms"] / ms for c, ms in zip(ceils, split_by_buf)],
+                     # memory.share_block's allocation-time fill probe of each block (TB/s; None: not probed)
+                     "probed_write_TBps": [(memory.block_rate(sb) or 0.0) / 1e12 or None for sb in share_bufs],
+                     "pool": memory.pool_stats()}
         # over the same buffers the timed average covers: mean of their ceilings
         ceiling = {"ms": float(np.mean([c["ms"] for c in ceils])), "grid": [c["grid"] for c in ceils],
                    "kernel": ceils[0]["kernel"], "buffers": len(ceils)}

@@ -9,6 +9,7 @@
 // "caller owns memory" contract is unchanged.  Host code, HIP runtime API only.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -74,7 +75,10 @@ extern "C" int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, 
   prop.location.type = hipMemLocationTypeDevice;
   prop.location.id = device;
   void* base = nullptr;
-  hipError_t e = hipMemAddressReserve(&base, b.span, 1ull << 21, nullptr, 0);
+  // DN_BLOCK_ALIGN_LOG2 (tuning build): the virtual range's alignment (placement probes)
+  uint64_t align = 1ull << 21;
+  if (const char* al = tune_env("DN_BLOCK_ALIGN_LOG2")) align = 1ull << std::atoi(al);
+  hipError_t e = hipMemAddressReserve(&base, b.span, align, nullptr, 0);
   if (e != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_alloc: reserve %llu B: %s",
                                         static_cast<unsigned long long>(b.span), hipGetErrorString(e));
   uint64_t mapped = 0;

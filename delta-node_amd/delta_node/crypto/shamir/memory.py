@@ -15,29 +15,47 @@ to an idle list (keyed by size, at most `POOL_IDLE_BYTES` held) and the next
 request of that size reuses it without new mappings; `empty_cache()` releases
 the idle blocks.  Below `CHUNKED_MIN_BYTES` (data that fits the caches, and
 where mapping costs more than it saves) `share_block` is torch.empty.
+
+Chunked blocks are not always fast either (r04q: 2 of 12 at 0.66-0.67 of
+8 TB/s for the split, the rest 0.72-0.79), and a block's write rate predicts
+its split (5.6-5.7 TB/s -> 0.66-0.67, >= 6.9 TB/s -> >= 0.78;
+profiles/r04/q/block_class.jsonl).  So a NEW share block of at least
+`PROBE_MIN_BYTES` is probed once (one timed fill) and kept only if it writes
+at >= `PROBE_KEEP` of the best rate this process has seen on the device;
+otherwise up to `PROBE_TRIES` blocks (at most `PROBE_BUDGET` bytes of them)
+are mapped and the fastest is kept (the others are freed after the choice, so
+a retry cannot get their pages back).
+The first large block on a device is the faster of two.
 """
 from __future__ import annotations
 
 import ctypes
 import math
 import threading
-from typing import Dict, List, Sequence, Tuple, Union
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 from . import _native
 
-__all__ = ["share_block", "chunked_block", "empty_cache", "granularity", "pool_stats"]
+__all__ = ["share_block", "chunked_block", "empty_cache", "granularity", "pool_stats", "block_rate"]
 
 CHUNK_BYTES = 2 << 20          # physical chunk of a pooled block
 CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
 POOL_IDLE_BYTES = 64 << 30     # most idle bytes the pool keeps mapped
+PROBE_MIN_BYTES = 256 << 20    # new share blocks from this size up are write-rate probed
+PROBE_TRIES = 4                # most blocks mapped for one request
+PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
+PROBE_BUDGET = 24 << 30        # most bytes mapped at once for one request's tries
 
 _lock = threading.Lock()
 _idle: Dict[Tuple[int, int, int], List[int]] = {}  # (device, nbytes, chunk) -> idle block pointers
 _idle_bytes = 0
-_stats = {"allocs": 0, "reuses": 0, "frees": 0}
+_stats = {"allocs": 0, "reuses": 0, "frees": 0, "probed": 0, "rejected": 0}
+_best_rate: Dict[int, float] = {}  # device -> fastest probed write rate (bytes/s)
+_rates: Dict[int, float] = {}      # block pointer -> its probed write rate
 
 
 def _free_ptr(ptr: int) -> None:
+    _rates.pop(ptr, None)
     _native.lib().dn_block_free(ptr)
     _stats["frees"] += 1
 
@@ -70,6 +88,81 @@ class _Block:
             pass
 
 
+class _View:
+    """A borrowed view of block memory for the probe (frees nothing)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+
+def _alloc_raw(nbytes: int, chunk_bytes: int, index: int) -> int:
+    p = ctypes.c_void_p()
+    rc = _native.lib().dn_block_alloc(nbytes, int(chunk_bytes), index, ctypes.byref(p))
+    if rc:
+        empty_cache()  # idle blocks of other sizes may hold the memory
+        rc = _native.lib().dn_block_alloc(nbytes, int(chunk_bytes), index, ctypes.byref(p))
+    _native.check(rc)
+    _stats["allocs"] += 1
+    return p.value
+
+
+def _write_rate(ptr: int, nbytes: int, dev) -> float:
+    """Bytes/s of one streaming fill of the block (best of two, after a first touch)."""
+    import torch
+
+    with torch.cuda.device(dev.index):
+        t = torch.as_tensor(_View(ptr, nbytes), device=dev)
+        stream = torch.cuda.current_stream()
+        t.fill_(0)
+        best = None
+        for _ in range(2):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            t.fill_(0)
+            e.record(stream)
+            e.synchronize()
+            ms = s.elapsed_time(e)
+            best = ms if best is None else min(best, ms)
+        del t
+    return nbytes / (best * 1e-3)
+
+
+def _alloc_probed(nbytes: int, chunk_bytes: int, dev) -> int:
+    """A new block, write-rate probed (see the module docstring)."""
+    best = _best_rate.get(dev.index)
+    cands: List[Tuple[float, int]] = []
+    tries = max(1, min(PROBE_TRIES, PROBE_BUDGET // max(1, nbytes)))
+    for k in range(tries):
+        try:
+            ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)
+        except RuntimeError:
+            if cands:  # out of memory for another try: keep the best so far
+                break
+            raise
+        rate = _write_rate(ptr, nbytes, dev)
+        _stats["probed"] += 1
+        cands.append((rate, ptr))
+        if best is None:
+            if k >= 1:  # the first large block on this device: the faster of two
+                break
+        elif rate >= PROBE_KEEP * best:
+            break
+    rate, keep = max(cands)
+    for r, p in cands:
+        if p != keep:
+            _free_ptr(p)
+            _stats["rejected"] += 1
+    _best_rate[dev.index] = max([best or 0.0] + [r for r, _ in cands])
+    _rates[keep] = rate
+    return keep
+
+
+def block_rate(t) -> Optional[float]:
+    """The probed write rate (bytes/s) of the block `t` starts at, if it was probed."""
+    return _rates.get(t.data_ptr())
+
+
 def granularity(device: int = 0) -> int:
     g = ctypes.c_uint64()
     _native.check(_native.lib().dn_block_granularity(device, ctypes.byref(g)))
@@ -86,10 +179,10 @@ def _device_index(device):
 
 
 def chunked_block(shape: Union[int, Sequence[int]], chunk_bytes: int = CHUNK_BYTES, device=None,
-                  pooled: bool = True):
+                  pooled: bool = True, probe: bool = False):
     """uint8 device tensor of `shape` whose memory is `chunk_bytes` physical
     chunks mapped back to back (from the idle pool when one of this size is
-    there)."""
+    there; probe: a new block is write-rate probed, see the module docstring)."""
     global _idle_bytes
     import torch
 
@@ -105,14 +198,10 @@ def chunked_block(shape: Union[int, Sequence[int]], chunk_bytes: int = CHUNK_BYT
             _idle_bytes -= nbytes
             _stats["reuses"] += 1
     if ptr is None:
-        p = ctypes.c_void_p()
-        rc = _native.lib().dn_block_alloc(nbytes, int(chunk_bytes), dev.index, ctypes.byref(p))
-        if rc:
-            empty_cache()  # idle blocks of other sizes may hold the memory
-            rc = _native.lib().dn_block_alloc(nbytes, int(chunk_bytes), dev.index, ctypes.byref(p))
-        _native.check(rc)
-        ptr = p.value
-        _stats["allocs"] += 1
+        if probe and nbytes >= PROBE_MIN_BYTES:
+            ptr = _alloc_probed(nbytes, chunk_bytes, dev)
+        else:
+            ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)
     blk = _Block(ptr, key, shape, pooled)
     with torch.cuda.device(dev.index):
         t = torch.as_tensor(blk, device=dev)
@@ -130,7 +219,7 @@ def share_block(shape: Union[int, Sequence[int]], device=None):
     shape = (int(shape),) if isinstance(shape, int) else tuple(int(s) for s in shape)
     if math.prod(shape) < CHUNKED_MIN_BYTES:
         return torch.empty(shape, dtype=torch.uint8, device=dev)
-    return chunked_block(shape, CHUNK_BYTES, dev)
+    return chunked_block(shape, CHUNK_BYTES, dev, probe=True)
 
 
 def empty_cache() -> None:

@@ -268,8 +268,10 @@ int dn_shamir_eval_at_host(const uint8_t* coeffs_be, const uint64_t* coeff_offse
  * reserved virtual range.  The split's rate depends on the physical pages of
  * its share block; this lets a caller choose the block's
  * composition.  dn_block_free synchronises the device, then unmaps and
- * releases every chunk.  Every other entry point keeps taking caller-owned
- * memory from any allocator.
+ * releases every chunk; the block's virtual range stays reserved for the life
+ * of the process (a new block mapped at a freed block's address had its bytes
+ * change under later allocations: DESIGN.md §5.2).  Every other entry point
+ * keeps taking caller-owned memory from any allocator.
  */
 int dn_block_granularity(int device, uint64_t* bytes);
 int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, void** ptr);

@@ -101,6 +101,34 @@ def test_freed_block_address_is_never_reused():
     assert st["idle_blocks"] == 0
 
 
+def test_share_block_write_rate_probe():
+    """A new share block of PROBE_MIN_BYTES or more is write-rate probed and
+    the kept block records its rate; the rejected tries are freed; an idle
+    block is reused without a new probe."""
+    memory.empty_cache()
+    s0 = memory.pool_stats()
+    nb = memory.PROBE_MIN_BYTES + (4 << 20)
+    b = memory.share_block((nb,), dev())
+    st = memory.pool_stats()
+    assert st["probed"] >= s0["probed"] + 1
+    assert st["allocs"] - s0["allocs"] == st["probed"] - s0["probed"]
+    assert st["rejected"] - s0["rejected"] == st["probed"] - s0["probed"] - 1
+    assert memory.block_rate(b) is not None and memory.block_rate(b) > 1e11
+    b.fill_(3)
+    assert int(b[-1].item()) == 3 and int(b[0].item()) == 3
+    ptr = b.data_ptr()
+    del b
+    gc.collect()
+    c = memory.share_block((nb,), dev())  # the idle block comes back, no new probe
+    assert c.data_ptr() == ptr and memory.pool_stats()["probed"] == st["probed"]
+    assert memory.block_rate(c) is not None
+    small = memory.share_block((memory.CHUNKED_MIN_BYTES + 4096,), dev())  # below PROBE_MIN_BYTES: not probed
+    assert memory.block_rate(small) is None
+    del c, small
+    gc.collect()
+    memory.empty_cache()
+
+
 def test_block_free_rejects_foreign_pointer():
     x = torch.empty(16, dtype=torch.uint8, device=dev())
     assert _native.lib().dn_block_free(x.data_ptr()) == _native.DN_ERR_ARG
