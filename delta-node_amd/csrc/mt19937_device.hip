@@ -115,6 +115,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The producer / consumer handoff: the ring half one wave wrote (ds_write)
+// or read (ds_read) in this step is complete before the other wave touches it
+// in the next, so a step ends with the LDS counter drained and s_barrier —
+// not __syncthreads(), whose workgroup-scope release also drains the global
+// stores: the consumer's 85 share stores per group would have to land before
+// every barrier (emission alone 1.18 vs 1.04 ms at 2^24, profiles/r04/s/).
+__device__ __forceinline__ void pc_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ------------------------------------------------------------------ jumps
 #ifndef DN_JUMP_TABLE_POS
 #define DN_JUMP_TABLE_POS 1  // jump table built per stream position (1) or per table word (0; A/B builds)
@@ -538,6 +548,16 @@ __device__ __forceinline__ void ring_run(uint32_t* Rg, const GenRing& g, uint32_
   if constexpr (NA % 3) ring_batch<NA % 3>(Rg, g, slot, lane, v);
 }
 
+// n appends, n known at run time (batches of three, then one or two).
+__device__ __forceinline__ void ring_run_rt(uint32_t* Rg, const GenRing& g, uint32_t& slot, uint32_t lane,
+                                            uint32_t n) {
+  uint32_t v[3];
+  uint32_t k = 0;
+  for (; k + 3u <= n; k += 3u) ring_batch<3>(Rg, g, slot, lane, v);
+  if (n - k == 2u) ring_batch<2>(Rg, g, slot, lane, v);
+  else if (n - k == 1u) ring_batch<1>(Rg, g, slot, lane, v);
+}
+
 // The window (624 raw words at stream positions [p_start - 624, p_start))
 // into the ring, with the mirror.
 __device__ __forceinline__ void ring_init(uint32_t* Rg, const GenRing& g, const uint32_t* win, uint32_t p_start,
@@ -631,12 +651,15 @@ __device__ __forceinline__ void mt_flag(const GenArgs& a) { __hip_atomic_store(a
 // 64 draws of one group (lane = draw c of this substream, raw words 17 c ..
 // 17 c + 16 of the group at `rb`): temper, +1, rejection test, tiled store.
 __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb, uint64_t qb, uint32_t rbm,
-                                          uint32_t c, uint32_t nloc, uint32_t lane) {
+                                          uint32_t c, uint32_t nloc, uint32_t lane, bool mid = false) {
   if (c >= nloc) return;
   uint32_t v[kLimbs];  // (the group's ring slice is 64 draws of 17 words)
   const uint32_t* w = rb + 17u * lane;
 #pragma unroll
-  for (int i = 0; i < kLimbs; ++i) v[i] = mt_temper(w[i]);
+  for (int i = 0; i < kLimbs; ++i) v[i] = w[i];
+  if (mid) pc_barrier();  // mt_gen_pc_kernel: the producer may now overwrite this group's slots
+#pragma unroll
+  for (int i = 0; i < kLimbs; ++i) v[i] = mt_temper(v[i]);
   v[16] >>= 23;
   uint32_t all = v[1];
 #pragma unroll
@@ -666,7 +689,7 @@ __device__ __forceinline__ void emit_group(const GenArgs& a, const uint32_t* rb,
 // rejection flagged) and secret s into the difference table c (fd_init).
 template <int T>
 __device__ __forceinline__ void emit_prepare(const GenArgs& a, const uint32_t* rb, uint32_t lane, uint64_t s,
-                                             uint32_t (&c)[T][kLimbs]) {
+                                             uint32_t (&c)[T][kLimbs], bool mid) {
   constexpr int TM1 = T - 1;
   const uint32_t* w = rb + 17u * TM1 * lane;
   if constexpr (TM1 % 2 == 0) {
@@ -679,6 +702,7 @@ __device__ __forceinline__ void emit_prepare(const GenArgs& a, const uint32_t* r
       const u32x2_t d = *reinterpret_cast<const u32x2_t*>(w + 2 * k);
       ww[2 * k] = d.x, ww[2 * k + 1] = d.y;
     }
+    if (mid) pc_barrier();  // mt_gen_pc_kernel: the producer may now overwrite this group's slots
 #pragma unroll
     for (int j = 1; j < T; ++j)
 #pragma unroll
@@ -687,7 +711,12 @@ __device__ __forceinline__ void emit_prepare(const GenArgs& a, const uint32_t* r
 #pragma unroll
     for (int j = 1; j < T; ++j)
 #pragma unroll
-      for (int i = 0; i < kLimbs; ++i) c[j][i] = mt_temper(w[17 * (j - 1) + i]);
+      for (int i = 0; i < kLimbs; ++i) c[j][i] = w[17 * (j - 1) + i];
+    if (mid) pc_barrier();
+#pragma unroll
+    for (int j = 1; j < T; ++j)
+#pragma unroll
+      for (int i = 0; i < kLimbs; ++i) c[j][i] = mt_temper(c[j][i]);
   }
 #pragma unroll
   for (int j = 1; j < T; ++j) {
@@ -709,7 +738,7 @@ __device__ __forceinline__ void emit_prepare(const GenArgs& a, const uint32_t* r
 
 template <int T, int SAUX, int NS, bool WHOLE>
 __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb, uint64_t ebase, uint32_t lane,
-                                           uint64_t s) {
+                                           uint64_t s, bool mid = false) {
   // ebase (the group's first element) is wave-uniform and a multiple of 64, so
   // the group's 64 elements share one tile: its index is a scalar and every
   // share store takes the tile's buffer descriptor from SGPRs (no per-lane
@@ -718,7 +747,7 @@ __device__ __forceinline__ void emit_split(const GenArgs& a, const uint32_t* rb,
   const uint64_t e = ebase + lane;
   if (!WHOLE && e >= a.n_elem) return;  // WHOLE: every element of the group is in the vector
   uint32_t c[T][kLimbs];
-  emit_prepare<T>(a, rb, lane, s, c);
+  emit_prepare<T>(a, rb, lane, s, c, mid);
   const uint32_t wl = static_cast<uint32_t>(e & 255u);
   if constexpr (NS > 0) {
 #pragma unroll
@@ -912,12 +941,13 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
 // substream runs between two emissions (r04i: full 1.02 ms, emission alone
 // 0.93, generation alone 0.50 at 2^24 3-of-5 on a share block).  Backward
 // substreams the same way downwards.  Same output and final state as
-// mt_gen_kernel<T> (T = 2, 3, 5; the coefficient draw keeps one wave).
+// mt_gen_kernel<T> (T = 2, 3, 5; T = 0 the coefficient draw, whose consumer
+// stores the tempered draws instead of splitting).
 // Dynamic LDS as mt_gen_kernel; registers for 4 waves per SIMD (8 workgroups
 // per CU, the most the rings' LDS allows at t <= 3), 2 at t = 5 (4 fit).
 template <int T, int SAUX = kNt, int NS = 0>
 __global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const GenArgs a) {
-  static_assert(T >= 2, "fused split only");
+  static_assert(T == 0 || T >= 2, "coefficient draw or fused split");
   extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
   const uint32_t lane = threadIdx.x & 63u;
   // (roles alternating with the workgroup's parity: no faster, profiles/r04/l/)
@@ -959,58 +989,106 @@ __global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const Ge
   const uint32_t group = a.ring / 2u;
   const uint64_t k0 = static_cast<uint64_t>(sub) * a.sub_draws;
   const uint32_t nloc = static_cast<uint32_t>(a.ncoef - k0 < a.sub_draws ? a.ncoef - k0 : a.sub_draws);
-  constexpr uint32_t gdraws = 64u * (T - 1);
+  constexpr uint32_t gdraws = T ? 64u * (T - 1) : 64u;
   const uint32_t ngroups = (nloc + gdraws - 1u) / gdraws;
   const uint64_t qb = k0 / static_cast<uint64_t>(a.tm1);
-  constexpr int kRun = 17 * (T - 1);
+  const uint32_t rbm = static_cast<uint32_t>(k0 - qb * static_cast<uint64_t>(a.tm1));
+  constexpr int kRun = 17 * (T ? T - 1 : 1);
   static_assert(kRun > 10, "a group holds the 640 words under the window");
   const bool prod = wid == 1u;
+  // The two waves run separate loops with the same number of barriers (one
+  // per step, ngroups + 1 steps), so the consumer's secrets stay in two
+  // registers by group parity as in mt_gen_kernel: no copy of a pending load
+  // (a copy waits vmcnt(0), i.e. for every share store in flight).
   if (!fwd) {
     // backward (whole groups, ngroups even; group gi in ring half gi % 2):
     // the producer fills the top group under the window, then per step
     // generates group gi - 1 while the consumer emits group gi
     const uint32_t M = a.ring;
-    uint32_t top = M - 640u;
     if (prod) {
+      uint32_t top = M - 640u;
       ring_init(R, g, win, p_start, lane);
       wave_sync();
       back_blocks<1, true, true>(R, M, M - 576u, lane, M - 624u);
       back_run<kRun - 10>(R, M, top, lane);
+      pc_barrier();
+      for (uint32_t gi = ngroups - 1u; gi > 0u; --gi) {
+        DN_PROBE_SKIP(a, 2u) back_run<kRun>(R, M, top, lane);
+        pc_barrier();
+      }
+      pc_barrier();
+      return;
     }
-    __syncthreads();
+    if constexpr (T == 0) {
+      pc_barrier();  // the top group is in the ring
+      for (uint32_t gi = ngroups - 1u;; --gi) {
+        DN_PROBE_SKIP(a, 1u) emit_group(a, R + (gi & 1u) * group, qb, rbm, 64u * gi + lane, nloc, lane);
+        pc_barrier();
+        if (gi == 0u) break;
+      }
+    } else {
     const uint64_t e0 = qb + lane;
     auto secret_of = [&](uint32_t gi) {
       return static_cast<uint64_t>(__builtin_nontemporal_load(a.secrets + e0 + 64u * gi));
     };
-    uint64_t secA = 0, secB = 0;
-    if (!prod) secA = secret_of(ngroups - 1u);
-    // step j emits group gi = ngroups - 1 - j (secret in cur, the next one's
-    // loaded into nxt before the stores) and generates group gi - 1
     auto bstep = [&](uint32_t gi, uint64_t cur, uint64_t& nxt) {
-      if (prod) {
-        if (gi > 0u) {
-          DN_PROBE_SKIP(a, 2u) back_run<kRun>(R, M, top, lane);
-        }
-      } else {
-        nxt = secret_of(gi ? gi - 1u : 0u);
-        DN_PROBE_SKIP(a, 1u)
-        emit_split<T, SAUX, NS, true>(a, R + (gi & 1u) * group, qb + 64u * gi, lane, cur);
-      }
-      __syncthreads();
+      nxt = secret_of(gi ? gi - 1u : 0u);
+      DN_PROBE_SKIP(a, 1u)
+      emit_split<T, SAUX, NS, true>(a, R + (gi & 1u) * group, qb + 64u * gi, lane, cur);
+      pc_barrier();
     };
+    uint64_t secA = secret_of(ngroups - 1u), secB = 0;
+    pc_barrier();  // the top group is in the ring
     for (uint32_t gi = ngroups - 1u;; gi -= 2u) {
       bstep(gi, secA, secB);
       bstep(gi - 1u, secB, secA);
       if (gi == 1u) break;
     }
-    if (!prod) asm volatile("" : : "v"(secA ^ secB));  // no load left in flight at the end
+    asm volatile("" : : "v"(secA ^ secB));  // no load left in flight at the end
+    }
     return;
   }
-  // forward: step i generates group i (producer) and emits group i - 1 (consumer)
+  // forward: step i generates group i (producer) and emits group i - 1 (consumer).
+  // Substream 0 starting inside the caller's array (p_start > 0) is the one
+  // place a run reaches past its group: run i ends with the first p_start
+  // words of group i + 1, whose ring slots are group i - 1's, which the
+  // consumer is emitting.  There each step has a second barrier: the consumer
+  // passes it once group i - 1's words are in its registers, the producer
+  // before the blocks from `kstar` on (the first one holding a word of group i
+  // + 1).
+  const bool mid = sub == 0u && p_start > 0u;
+  const uint32_t kstar = mid ? (group - p_start) / 64u : static_cast<uint32_t>(kRun);
+#ifdef DN_TUNING
+  const bool skip_emit = (a.probe & 1u) != 0u, skip_gen = (a.probe & 2u) != 0u;
+#else
+  constexpr bool skip_emit = false, skip_gen = false;
+#endif
   if (prod) {
     ring_init(R, g, win, p_start, lane);
     wave_sync();
+    for (uint32_t i = 0; i < ngroups; ++i) {
+      if (mid) {
+        if (!skip_gen) ring_run_rt(R, g, slot, lane, kstar);
+        pc_barrier();
+        if (!skip_gen) ring_run_rt(R, g, slot, lane, static_cast<uint32_t>(kRun) - kstar);
+      } else if (!skip_gen) {
+        ring_run<kRun>(R, g, slot, lane);
+      }
+      pc_barrier();
+    }
+    if (mid) pc_barrier();
+    pc_barrier();
+    return;
   }
+  if constexpr (T == 0) {
+    if (mid) pc_barrier();
+    pc_barrier();  // group 0 is in the ring
+    for (uint32_t gi = 0; gi < ngroups; ++gi) {
+      if (!skip_emit) emit_group(a, R + g.o + g.delta + (gi & 1u) * group, qb, rbm, 64u * gi + lane, nloc, lane, mid);
+      else if (mid) pc_barrier();
+      pc_barrier();
+    }
+  } else {
   const uint64_t e0 = qb + lane;
   const uint64_t elast = a.n_elem - 1u;
   auto secret_of = [&](uint32_t gi) {
@@ -1019,36 +1097,33 @@ __global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const Ge
   };
   const uint64_t rem = a.n_elem - qb;
   const uint32_t nfull = rem >= 64ull * ngroups ? ngroups : static_cast<uint32_t>(rem / 64u);
-  // the consumer's secrets: group i - 1's in cur, group i's loaded into nxt
-  // before the stores (two registers by parity, as mt_gen_kernel)
-  auto fstep = [&](uint32_t i, uint64_t cur, uint64_t& nxt) {
-    if (prod) {
-      if (i < ngroups) {
-        DN_PROBE_SKIP(a, 2u) ring_run<kRun>(R, g, slot, lane);
-      }
-    } else if (i >= 1u) {
-      const uint32_t gi = i - 1u;
-      nxt = secret_of(i);
-      if (gi < nfull) {
-        DN_PROBE_SKIP(a, 1u)
-        emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
-      } else {  // the vector's last, partial group
-        emit_split<T, SAUX, NS, false>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur);
-      }
-    }
-    __syncthreads();
+  auto cstep = [&](uint32_t gi, uint64_t cur, uint64_t& nxt) {
+    nxt = secret_of(gi + 1u);
+    if (!skip_emit)
+      emit_split<T, SAUX, NS, true>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, cur, mid);
+    else if (mid)
+      pc_barrier();
+    pc_barrier();
   };
-  uint64_t secA = 0, secB = 0;
-  if (!prod) secA = secret_of(0);
-  fstep(0u, 0u, secB);  // group 0 generated; nothing to emit (secB untouched)
-  uint32_t i = 1u;
-  for (; i + 1u <= ngroups; i += 2u) {
-    fstep(i, secA, secB);
-    if (i + 1u > ngroups) break;
-    fstep(i + 1u, secB, secA);
+  uint64_t secA = secret_of(0), secB = 0;
+  if (mid) pc_barrier();
+  pc_barrier();  // group 0 is in the ring
+  uint32_t gi = 0;
+  for (; gi + 1u < nfull; gi += 2u) {
+    cstep(gi, secA, secB);
+    cstep(gi + 1u, secB, secA);
   }
-  if (i <= ngroups) fstep(i, secA, secB);
-  if (!prod) asm volatile("" : : "v"(secA ^ secB));
+  if (gi < nfull) {
+    cstep(gi, secA, secB);
+    ++gi;
+  }
+  if (gi < ngroups) {  // the vector's last, partial group
+    emit_split<T, SAUX, NS, false>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, secret_of(gi),
+                                   mid);
+    pc_barrier();
+  }
+  asm volatile("" : : "v"(secA ^ secB));
+  }
 }
 
 uint64_t mt_subs(uint64_t ncoef) {
@@ -1628,13 +1703,15 @@ void launch_gen(GenArgs& ga, hipStream_t s) {
   // the headline 3-of-5: straight-line share stores (see mt_gen_kernel), sc1
   // rather than non-temporal: 2.2 % faster on two buffers of one process
   // (profiles/r03/ab/mt_store_aux_ns5.json)
-  // Two waves per substream pay off while the one-wave kernel would hold at
-  // most one wave per SIMD (S + 1 <= 4 per CU): make_shares_vec 2^20 / 2^16 /
-  // 2^12 -12 / -8 / -3 %; with every CU's 8 ring slots taken (2^24: S + 1 =
-  // 2049) both are bound by the share writes and the one-wave kernel was 9 %
-  // faster (profiles/r04/l/).
-  if constexpr (T >= 2 && DN_MT_PC) {
-    if (static_cast<uint64_t>(ga.S) + 1u <= 4u * static_cast<uint64_t>(device_cu_count())) {
+  // Generation and emission on two waves per substream (mt_gen_pc_kernel):
+  // at 2^24 the kernel runs at its emission-only time (0.92 vs 1.01 ms for
+  // the one-wave kernel on a share block, profiles/r04/t/), at 2^20 / 2^16 /
+  // 2^12 make_shares_vec -12 / -8 / -3 % (profiles/r04/l/).
+  if constexpr (DN_MT_PC) {
+    // DN_MT_PC_FORCE (tuning build): 0 = the one-wave kernel (A/B)
+    const char* pf = tune_env("DN_MT_PC_FORCE");
+    const bool pc = !(pf && pf[0] == '0');
+    if (pc) {
       if (T == 3 && ga.n_shares == 5)
         hipLaunchKernelGGL((mt_gen_pc_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(128), lds_words * 4u, s,
                            ga);

@@ -33,8 +33,13 @@ blocks = [("share_block", memory.share_block((5, vb), dev)),
 ss = shamir.SecretShare(3)
 ss.random.seed(5)
 order = []
+BACKS = os.environ.get("BACKS", "1,0,2").split(",")
+PCS = os.environ.get("PCS", "").split(",") if os.environ.get("PCS") else [None]
 for bi, (kind, blk) in enumerate(blocks):
-    for back in ("1", "0", "2"):
+  for pc in PCS:
+    if pc is not None:
+        os.environ["DN_MT_PC_FORCE"] = pc
+    for back in BACKS:
         os.environ["DN_MT_BACK"] = back
         for probe in ("0", "1", "2"):
             os.environ["DN_MT_PROBE"] = probe
@@ -42,9 +47,14 @@ for bi, (kind, blk) in enumerate(blocks):
                 ss.make_shares_vec(sec, 5, out=blk)
                 torch.cuda.synchronize()
                 time.sleep(0.001)
-            order.append({"block": bi, "kind": kind, "back": int(back), "probe": int(probe), "calls": REPS})
+            order.append({"block": bi, "kind": kind, "back": int(back), "probe": int(probe), "calls": REPS,
+                          "pc": pc})
 os.environ.pop("DN_MT_PROBE")
 os.environ.pop("DN_MT_BACK")
+os.environ.pop("DN_MT_PC_FORCE", None)
+if os.environ.get("NO_FG"):
+    print(json.dumps({"order": order}))
+    sys.exit(0)
 # the pair boundary (mt_sub_range): forward groups per pair of 2 x 128 at t = 3;
 # every split must give the same shares and the same final state
 blk = blocks[0][1]

@@ -13,7 +13,7 @@ for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if "mt_gen_kernel<3" in n:
+        if "mt_gen_kernel<3" in n or "mt_gen_pc_kernel<3" in n:
             gen.append((int(r["Start_Timestamp"]), dur))
         elif "mt_jump_kernel" in n:
             jumps.append((int(r["Start_Timestamp"]), dur))

@@ -444,6 +444,37 @@ def test_fused_draw_split_equals_draw_then_split(t, n, N):
     assert a.random.getstate() == b.random.getstate()
 
 
+@pytest.mark.parametrize("pre", [1, 100, 333, 560, 600, 623])
+@pytest.mark.parametrize("kind", ["fused", "draw"])
+def test_two_wave_generation_substream0_inside_callers_array(pre, kind):
+    """Substream 0 starts inside the caller's array (624 - idx words already
+    there): in mt_gen_pc_kernel its runs reach into the next group's ring
+    slots, which the other wave is emitting from (the mid-step barrier).  The
+    fused split (3-of-5) and the coefficient draw at sizes of one to thousands
+    of substreams, every in-array offset class (p_start 1..624, a multiple of
+    64 at pre = 560), against the host draw."""
+    for n in (1000, 40000, (1 << 20) + 77):
+        a, b = shamir.SecretShare(3), shamir.SecretShare(3)
+        a.random.seed(pre * 7 + n)
+        b.random.seed(pre * 7 + n)
+        a.random.getrandbits(32 * pre)
+        b.random.getrandbits(32 * pre)
+        if kind == "fused":
+            sec = torch.randint(-(1 << 62), 1 << 62, (n,), dtype=torch.int64, device=dev())
+            got = a.make_shares_vec(sec, 5)
+            co = torch.from_numpy(_native.mt_draw_coeffs(b.random, n, 2)).to(dev())  # the host draw
+            want = torch.empty_like(got)
+            _native.split_u64(sec, co, want, n, 3, 5)
+        else:
+            got = torch.zeros((2, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+            assert _native.mt_draw_coeffs_device(a.random, n, 2, got)
+            want = torch.from_numpy(_native.mt_draw_coeffs(b.random, n, 2)).to(dev())
+        g, w = got.cpu().numpy(), want.cpu().numpy()  # the elements (tile padding is never written)
+        for r in range(g.shape[0]):
+            assert np.array_equal(field.vec_to_limbs(g[r], n), field.vec_to_limbs(w[r], n)), (pre, kind, n, r)
+        assert a.random.getstate() == b.random.getstate()
+
+
 def test_fused_draw_split_declines_and_falls_back():
     """t outside {2, 3, 5} (and n beyond forward differences) is declined with
     the state untouched; make_shares_vec then draws and splits, and a forced
