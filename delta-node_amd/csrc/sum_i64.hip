@@ -5,6 +5,8 @@
 // per element.  `out` may alias inputs[0] (accumulate in place).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dn_internal.hpp"
 #include "dn_mask.h"
 
@@ -61,4 +63,39 @@ extern "C" int dn_i64_sum(const int64_t* const* inputs, int k, int64_t* out, uin
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_i64_sum: %s", hipGetErrorString(err));
   return DN_OK;
+}
+
+// ---- share-block write probe (memory.share_block) ---------------------------
+// Writes zeros over `rows` rows of `row_bytes` (a multiple of the 16896-byte
+// tile) in the order a split writes a share block: per 256-element tile, that
+// tile's slice of every row, 16-B non-temporal stores (a wave per tile).  A
+// block's rate under this pattern predicts its split; a linear fill does not
+// (profiles/r04/y/).
+namespace {
+typedef uint32_t u32x4_p __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) block_probe_kernel(uint8_t* p, uint32_t rows, uint64_t row_bytes,
+                                                          uint64_t ntiles) {
+  constexpr uint32_t kTileB = 66u * 256u;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * 4u;
+  const u32x4_p z = {0u, 0u, 0u, 0u};
+  for (uint64_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6)); t < ntiles; t += nw)
+    for (uint32_t r = 0; r < rows; ++r) {
+      u32x4_p* q = reinterpret_cast<u32x4_p*>(p + r * row_bytes + t * kTileB);
+#pragma unroll 4
+      for (uint32_t o = lane; o < kTileB / 16u; o += 64u) __builtin_nontemporal_store(z, q + o);
+    }
+}
+}  // namespace
+
+extern "C" int dn_block_probe_rows(void* ptr, uint32_t rows, uint64_t row_bytes, void* stream) {
+  constexpr uint64_t kTileB = 66u * 256u;
+  if (!ptr || rows == 0 || row_bytes == 0 || row_bytes % kTileB)
+    return dn::set_error(DN_ERR_ARG, "dn_block_probe_rows: rows of whole 16896-byte tiles");
+  const uint64_t ntiles = row_bytes / kTileB;
+  const uint64_t g = std::min<uint64_t>(16384u, (ntiles + 3u) / 4u);
+  hipLaunchKernelGGL(block_probe_kernel, dim3(static_cast<uint32_t>(g)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), static_cast<uint8_t*>(ptr), rows, row_bytes, ntiles);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DN_OK : dn::set_error(DN_ERR_HIP, "dn_block_probe_rows: %s", hipGetErrorString(e));
 }

@@ -20,8 +20,10 @@ Chunked blocks are not always fast either (r04q: 2 of 12 at 0.66-0.67 of
 8 TB/s for the split, the rest 0.72-0.79), and a block's write rate predicts
 its split (5.6-5.7 TB/s -> 0.66-0.67, >= 6.9 TB/s -> >= 0.78;
 profiles/r04/q/block_class.jsonl).  So a NEW share block of at least
-`PROBE_MIN_BYTES` is probed once (one timed fill) and kept only if it writes
-at >= `PROBE_KEEP` of the best rate this process has seen on the device;
+`PROBE_MIN_BYTES` is probed once (one timed write in the split's order:
+per tile, every row's slice) and kept only if it writes
+at >= `PROBE_KEEP` of the best rate this process has seen on the device
+for blocks of that many rows;
 otherwise up to `PROBE_TRIES` blocks (at most `PROBE_BUDGET` bytes of them)
 are mapped and the fastest is kept (the others are freed after the choice, so
 a retry cannot get their pages back).
@@ -50,7 +52,7 @@ _lock = threading.Lock()
 _idle: Dict[Tuple[int, int, int], List[int]] = {}  # (device, nbytes, chunk) -> idle block pointers
 _idle_bytes = 0
 _stats = {"allocs": 0, "reuses": 0, "frees": 0, "probed": 0, "rejected": 0}
-_best_rate: Dict[int, float] = {}  # device -> fastest probed write rate (bytes/s)
+_best_rate: Dict[Tuple[int, int], float] = {}  # (device, rows) -> fastest probed write rate (bytes/s)
 _rates: Dict[int, float] = {}      # block pointer -> its probed write rate
 
 
@@ -107,30 +109,46 @@ def _alloc_raw(nbytes: int, chunk_bytes: int, index: int) -> int:
     return p.value
 
 
-def _write_rate(ptr: int, nbytes: int, dev) -> float:
-    """Bytes/s of one streaming fill of the block (best of two, after a first touch)."""
+def _write_rate(ptr: int, nbytes: int, dev, shape) -> float:
+    """Bytes/s of writing the block (best of two, after a first touch): for a
+    block of rows of whole tiles (a share or coefficient block) in the order
+    a split writes it (dn_block_probe_rows: per tile, every row's slice) —
+    a linear fill ran at the same rate on blocks whose split differed by
+    20 % (profiles/r04/x/ vs r04/y/); else one linear fill."""
     import torch
 
+    from . import field
+
+    rows = int(shape[0]) if len(shape) == 2 else 0
+    tiled = rows > 0 and int(shape[1]) % field.TILE_BYTES == 0
     with torch.cuda.device(dev.index):
         t = torch.as_tensor(_View(ptr, nbytes), device=dev)
         stream = torch.cuda.current_stream()
-        t.fill_(0)
+
+        def write():
+            if tiled:
+                _native.check(_native.lib().dn_block_probe_rows(ptr, rows, int(shape[1]), stream.cuda_stream))
+            else:
+                t.fill_(0)
+
+        write()
         best = None
         for _ in range(2):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(stream)
-            t.fill_(0)
+            write()
             e.record(stream)
             e.synchronize()
             ms = s.elapsed_time(e)
             best = ms if best is None else min(best, ms)
         del t
-    return nbytes / (best * 1e-3)
+    return (rows * int(shape[1]) if tiled else nbytes) / (best * 1e-3)
 
 
-def _alloc_probed(nbytes: int, chunk_bytes: int, dev) -> int:
+def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
     """A new block, write-rate probed (see the module docstring)."""
-    best = _best_rate.get(dev.index)
+    kind = (dev.index, int(shape[0]) if len(shape) == 2 else 0)  # rates compare within one block shape class
+    best = _best_rate.get(kind)
     cands: List[Tuple[float, int]] = []
     tries = max(1, min(PROBE_TRIES, PROBE_BUDGET // max(1, nbytes)))
     for k in range(tries):
@@ -140,7 +158,7 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev) -> int:
             if cands:  # out of memory for another try: keep the best so far
                 break
             raise
-        rate = _write_rate(ptr, nbytes, dev)
+        rate = _write_rate(ptr, nbytes, dev, shape)
         _stats["probed"] += 1
         cands.append((rate, ptr))
         if best is None:
@@ -153,7 +171,7 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev) -> int:
         if p != keep:
             _free_ptr(p)
             _stats["rejected"] += 1
-    _best_rate[dev.index] = max([best or 0.0] + [r for r, _ in cands])
+    _best_rate[kind] = max([best or 0.0] + [r for r, _ in cands])
     _rates[keep] = rate
     return keep
 
@@ -199,7 +217,7 @@ def chunked_block(shape: Union[int, Sequence[int]], chunk_bytes: int = CHUNK_BYT
             _stats["reuses"] += 1
     if ptr is None:
         if probe and nbytes >= PROBE_MIN_BYTES:
-            ptr = _alloc_probed(nbytes, chunk_bytes, dev)
+            ptr = _alloc_probed(nbytes, chunk_bytes, dev, shape)
         else:
             ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)
     blk = _Block(ptr, key, shape, pooled)

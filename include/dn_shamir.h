@@ -278,6 +278,14 @@ int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, void** ptr)
 int dn_block_free(void* ptr);
 
 /*
+ * Device, async on `stream`.  Zero `rows` rows of `row_bytes` (whole
+ * 16896-byte tiles) at `ptr` in the order a split writes a share block (per
+ * tile, every row's slice): the allocator times it to judge a new block's
+ * placement (memory.share_block).
+ */
+int dn_block_probe_rows(void* ptr, uint32_t rows, uint64_t row_bytes, void* stream);
+
+/*
  * Host.  Advance a CPython MT19937 state by `words` 32-bit outputs (as
  * `words` getrandbits(32) calls would) by jump-ahead instead of stepping.
  */
