@@ -24,7 +24,7 @@ for name in ("pmc_fetch", "pmc_write", "pmc_req"):
             kn = row["Kernel_Name"]
             k = ("split" if "split_kernel" in kn else
                  "reconstruct" if "reconstruct_kernel" in kn else
-                 "fused_draw_split" if "mt_gen_kernel<3" in kn else
+                 "fused_draw_split" if ("mt_gen_kernel<3" in kn or "mt_gen_pc_kernel<3" in kn) else
                  "mask_accumulate" if "bounded_acc_kernel" in kn else None)
             if k:
                 vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
