@@ -829,6 +829,54 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
             "equal_draw_then_split_and_state": ok, "fused_ms_by_size": by_size}
 
 
+def reference_digest_equal(block, n: int, name: str) -> bool:
+    """SHA-256 checksum of checksums of a share block's limb planes against
+    the reference-generated digest `name` (tests/golden/make_golden.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden.fixtures import chunk_digests, combine_digests, manifest
+
+    from delta_node.crypto.shamir import field
+
+    want = [d for d in manifest()["digests"] if d["name"] == name][0]["digest"]
+    h = block.cpu().numpy()
+    planes = np.stack([field.vec_to_planes(h[s], n) for s in range(h.shape[0])])
+    del h
+    return combine_digests(chunk_digests(planes)) == want
+
+
+def _child_json(cmd, timeout: float) -> dict:
+    """Run `cmd` as a fresh child process; its last JSON line (or the failure)."""
+    import subprocess
+
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timeout after {timeout} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode or not lines:
+        return {"error": f"exit {r.returncode}: {r.stderr[-400:]}"}
+    return json.loads(lines[-1])
+
+
+def cold_row(log2n: int) -> dict:
+    """The first make_shares_vec of a fresh process (scripts/cold_call.py), and
+    BASELINE config 5's first round in a fresh runner/peer pair
+    (scripts/e2e_round.py --cold): what a reference round, which splits once
+    (runner/horizontal/agg.py:142-153), actually pays.  Every other row is warm."""
+    py = sys.executable
+    e2e = _child_json([py, "scripts/cold_call.py", "--log2n", str(log2n), "--mode", "e2e"], 300)
+    phases = _child_json([py, "scripts/cold_call.py", "--log2n", str(log2n), "--mode", "phases"], 300)
+    c5 = _child_json([py, "scripts/e2e_round.py", "--cold", "--rounds", "1", "--coeffs", "mt",
+                      "--log2n", str(log2n), "--port", str(free_port())], 600)
+    return {"workload": f"first make_shares_vec(2^{log2n} int64, 5) of a fresh process, secrets already on "
+                        "the device; wall time to return",
+            "cold_ms": e2e.get("first_ms"), "warm_after_ms": e2e.get("second_ms"), "first_call": e2e,
+            "phases": phases,
+            "config5_first_round": {k: c5.get(k) for k in ("wall_s", "input_MBps", "pack_s", "h2d_s", "split_s",
+                                                           "encode_d2h_s", "post_tail_s", "peer_verified", "error")
+                                    if k in c5}}
+
+
 def byte_api_row(budget_s: float = 2.0) -> dict:
     """The call sites the reference actually has (runner/horizontal/agg.py:142-153,
     coord/horizontal/agg.py:296,330,362): make_shares of one 32-byte secret into
@@ -945,6 +993,8 @@ def main():
     ap.add_argument("--config4-log2n", type=int, default=26, help="config 4 total elements = 2^this")
     ap.add_argument("--config5", type=int, default=1, help="also run BASELINE config 5 (end-to-end round over "
                                                             "loopback HTTP to a second process; N=1 only)")
+    ap.add_argument("--cold", type=int, default=1, help="also time the first make_shares_vec / config-5 round "
+                                                         "of fresh processes (with --rows; N=1 only)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ:
@@ -1070,7 +1120,13 @@ def main():
     got = np.stack([field.vec_to_limbs(shares[x, : field.vec_bytes(sample)].cpu().numpy(), sample) for x in range(n)])
     oracle_ok = bool(np.array_equal(got, want))
     bufs_equal = all(bool(torch.equal(sb, shares)) for sb in share_bufs)
-    all_ok = roundtrip and oracle_ok and bufs_equal
+    # the headline workload IS the reference's split_t3n5_2e24 digest case
+    # (secrets_int64(1, 2^24), random.seed(1)): the timed share block's digest
+    # against the one the reference itself produced (tests/golden/manifest.json)
+    ref_digest_ok = None
+    if world == 1 and N_total == (1 << 24) and (t, n) == (3, 5):
+        ref_digest_ok = reference_digest_equal(shares, N, "split_t3n5_2e24")
+    all_ok = roundtrip and oracle_ok and bufs_equal and ref_digest_ok is not False
     if dist_on:  # every rank's parity, not only rank 0's
         fl = torch.tensor([int(all_ok)], dtype=torch.int32, device=cdev)
         torch.distributed.all_reduce(fl, op=torch.distributed.ReduceOp.MIN)
@@ -1186,7 +1242,7 @@ def main():
                         **recon_ceiling, "GBps": recon_bytes / (recon_ceiling["ms"] * 1e-3) / 1e9,
                         "reconstruct_frac_of_ceiling": recon_ceiling["ms"] / recon_ms}},
         "parity": {"roundtrip_equal": roundtrip, "c_oracle_sample_equal": oracle_ok, "sample": sample,
-                   "all_ranks_ok": all_ok},
+                   "reference_digest_equal": ref_digest_ok, "all_ranks_ok": all_ok},
     }
     if weak:
         line["weak_scaling"] = weak
@@ -1200,6 +1256,8 @@ def main():
     if args.rows and world == 1:
         line["rows"] = rows_bench(dev, args.log2n)
         line["rows"]["draw_split"] = draw_split_row(dev, args.log2n)
+        if args.cold:
+            line["rows"]["draw_split"]["cold"] = cold_row(args.log2n)
         line["rows"]["byte_api"] = byte_api_row()
     if args.config5 and world == 1:
         line["config5"] = config5_bench(args.log2n)

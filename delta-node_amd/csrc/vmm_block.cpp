@@ -19,11 +19,35 @@
 namespace dn {
 namespace {
 
+// One recorded use of a block: an event recorded on `stream` after the work
+// that touched the block there (dn_block_record).
+struct Use {
+  hipStream_t stream = nullptr;
+  hipEvent_t event = nullptr;
+  bool pending = false;  // recorded since the block's last dn_block_acquire
+};
+
 struct Block {
   uint64_t span = 0;  // reserved / mapped bytes
   uint64_t chunk = 0;
+  int device = 0;
   std::vector<hipMemGenericAllocationHandle_t> handles;
+  std::vector<Use> uses;  // one event per stream the block was used on (kept for re-recording)
 };
+
+// Runs `f` with `device` current and restores the caller's device.
+template <class F>
+hipError_t on_device(int device, F&& f) {
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != device) {
+    const hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return e;
+  }
+  const hipError_t r = f();
+  if (prev != device && prev >= 0) (void)hipSetDevice(prev);
+  return r;
+}
 
 std::mutex& blocks_mutex() {
   static std::mutex* m = new std::mutex;  // never destroyed (the runtime may go first)
@@ -34,11 +58,10 @@ std::map<uintptr_t, Block>& blocks() {
   return *b;
 }
 
-void release(void* base, Block& b, uint64_t mapped) {
-  if (mapped) (void)hipMemUnmap(base, mapped);
-  (void)hipMemAddressFree(base, b.span);
-  for (auto h : b.handles) (void)hipMemRelease(h);
-  b.handles.clear();
+// Looks a block up by its base pointer (callers hold blocks_mutex()).
+Block* find_block(void* ptr) {
+  auto it = blocks().find(reinterpret_cast<uintptr_t>(ptr));
+  return it == blocks().end() ? nullptr : &it->second;
 }
 
 }  // namespace
@@ -70,6 +93,7 @@ extern "C" int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, 
   Block b;
   b.span = nch * chunk;
   b.chunk = chunk;
+  b.device = device;
   hipMemAllocationProp prop{};
   prop.type = hipMemAllocationTypePinned;
   prop.location.type = hipMemLocationTypeDevice;
@@ -99,14 +123,87 @@ extern "C" int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, 
   }
   if (e != hipSuccess) {
     // a partial mapping is unmapped piece by piece (one unmap per mapped chunk)
+    // and its chunks released; the virtual range stays reserved (retired, as
+    // in dn_block_free: no later block is placed where these mappings were)
     for (uint64_t off = 0; off < mapped; off += chunk) (void)hipMemUnmap(static_cast<uint8_t*>(base) + off, chunk);
-    release(base, b, 0);
+    for (auto h : b.handles) (void)hipMemRelease(h);
     return set_error(DN_ERR_HIP, "dn_block_alloc: %llu B in %llu-B chunks: %s", static_cast<unsigned long long>(bytes),
                      static_cast<unsigned long long>(chunk), hipGetErrorString(e));
   }
   std::lock_guard<std::mutex> g(blocks_mutex());
   blocks()[reinterpret_cast<uintptr_t>(base)] = std::move(b);
   *ptr = base;
+  return DN_OK;
+}
+
+// ---- stream-ordered reuse (memory.py's pool) --------------------------------
+// A block that goes idle records an event on every stream that used it; a
+// request on stream S may take it at once when every recorded event is on S
+// (stream order covers it) or has completed, and dn_block_acquire can make S
+// wait for the others instead.  This is torch's caching-allocator rule
+// (record_stream), kept per block here because the pool lives outside torch.
+
+extern "C" int dn_block_record(void* ptr, void* stream) {
+  std::lock_guard<std::mutex> g(blocks_mutex());
+  Block* b = find_block(ptr);
+  if (!b) return set_error(DN_ERR_ARG, "dn_block_record: not a dn_block_alloc pointer");
+  const auto s = static_cast<hipStream_t>(stream);
+  Use* u = nullptr;
+  for (auto& x : b->uses)
+    if (x.stream == s) u = &x;
+  const hipError_t e = on_device(b->device, [&]() -> hipError_t {
+    if (!u) {
+      hipEvent_t ev = nullptr;
+      const hipError_t c = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (c != hipSuccess) return c;
+      b->uses.push_back(Use{s, ev, false});
+      u = &b->uses.back();
+    }
+    return hipEventRecord(u->event, s);
+  });
+  if (e != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_record: %s", hipGetErrorString(e));
+  u->pending = true;
+  return DN_OK;
+}
+
+extern "C" int dn_block_ready(void* ptr, void* stream, int* ready) {
+  if (!ready) return set_error(DN_ERR_ARG, "dn_block_ready: null pointer");
+  std::lock_guard<std::mutex> g(blocks_mutex());
+  Block* b = find_block(ptr);
+  if (!b) return set_error(DN_ERR_ARG, "dn_block_ready: not a dn_block_alloc pointer");
+  *ready = 1;
+  for (auto& u : b->uses) {
+    if (!u.pending || u.stream == static_cast<hipStream_t>(stream)) continue;
+    const hipError_t q = hipEventQuery(u.event);
+    if (q == hipErrorNotReady) {
+      *ready = 0;
+      return DN_OK;
+    }
+    if (q != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_ready: %s", hipGetErrorString(q));
+    u.pending = false;  // completed: nothing left to order against
+  }
+  return DN_OK;
+}
+
+extern "C" int dn_block_acquire(void* ptr, void* stream, int wait) {
+  std::lock_guard<std::mutex> g(blocks_mutex());
+  Block* b = find_block(ptr);
+  if (!b) return set_error(DN_ERR_ARG, "dn_block_acquire: not a dn_block_alloc pointer");
+  const auto s = static_cast<hipStream_t>(stream);
+  for (auto& u : b->uses) {
+    if (!u.pending) continue;
+    if (u.stream != s) {
+      if (!wait) {
+        const hipError_t q = hipEventQuery(u.event);
+        if (q == hipErrorNotReady) return set_error(DN_ERR_RETRY, "dn_block_acquire: still in use on another stream");
+        if (q != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_acquire: %s", hipGetErrorString(q));
+      } else {
+        const hipError_t e = on_device(b->device, [&] { return hipStreamWaitEvent(s, u.event, 0); });
+        if (e != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_acquire: %s", hipGetErrorString(e));
+      }
+    }
+    u.pending = false;
+  }
   return DN_OK;
 }
 
@@ -129,17 +226,26 @@ extern "C" int dn_block_free(void* ptr) {
     b = std::move(it->second);
     blocks().erase(it);
   }
-  // kernels still using the block finish before its pages go (a free is rare)
-  hipError_t first = hipDeviceSynchronize();
-  // per-chunk unmap: every mapping was made chunk by chunk
-  for (uint64_t off = 0; off < b.span; off += b.chunk) {
-    const hipError_t e = hipMemUnmap(static_cast<uint8_t*>(ptr) + off, b.chunk);
-    if (first == hipSuccess) first = e;
-  }
-  for (auto h : b.handles) {
-    const hipError_t e = hipMemRelease(h);
-    if (first == hipSuccess) first = e;
-  }
+  // work still using the block finishes before its pages go: the events its
+  // uses recorded (dn_block_record), or — a block nobody recorded, e.g. a C
+  // caller's — everything queued on the block's own device
+  bool recorded = false;
+  for (auto& u : b.uses) recorded |= u.pending;
+  const hipError_t first = on_device(b.device, [&]() -> hipError_t {
+    hipError_t r = recorded ? hipSuccess : hipDeviceSynchronize();
+    auto keep = [&r](hipError_t e) {
+      if (r == hipSuccess) r = e;
+    };
+    for (auto& u : b.uses) {
+      if (u.pending) keep(hipEventSynchronize(u.event));
+      (void)hipEventDestroy(u.event);
+    }
+    // per-chunk unmap: every mapping was made chunk by chunk
+    for (uint64_t off = 0; off < b.span; off += b.chunk) keep(hipMemUnmap(static_cast<uint8_t*>(ptr) + off, b.chunk));
+    for (auto h : b.handles) keep(hipMemRelease(h));
+    return r;
+  });
+  b.uses.clear();
   b.handles.clear();
   if (first != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_free: %s", hipGetErrorString(first));
   return DN_OK;

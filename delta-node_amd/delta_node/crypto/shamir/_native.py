@@ -47,6 +47,7 @@ EXPORTS = (
     "dn_mt19937_device_scratch_bytes", "dn_mt19937_draw_coeffs_device", "dn_mt19937_skip",
     "dn_mt19937_split_device", "dn_mt19937_split_supported", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
     "dn_shamir_eval_at_host", "dn_block_granularity", "dn_block_alloc", "dn_block_free", "dn_block_probe_rows",
+    "dn_block_record", "dn_block_ready", "dn_block_acquire",
 )
 
 
@@ -159,6 +160,12 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_block_alloc.argtypes = [u64, u64, i32, ctypes.POINTER(ctypes.c_void_p)]
     L.dn_block_free.restype = i32
     L.dn_block_free.argtypes = [vp]
+    L.dn_block_record.restype = i32
+    L.dn_block_record.argtypes = [vp, vp]
+    L.dn_block_ready.restype = i32
+    L.dn_block_ready.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
+    L.dn_block_acquire.restype = i32
+    L.dn_block_acquire.argtypes = [vp, vp, i32]
     L.dn_block_probe_rows.restype = i32
     L.dn_block_probe_rows.argtypes = [vp, ctypes.c_uint32, u64, vp]
     L.dn_mt19937_skip.restype = i32

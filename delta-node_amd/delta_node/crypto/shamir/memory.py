@@ -11,10 +11,26 @@ API allocates the share blocks it returns here (`share_block`), and callers
 may too.  Every API keeps accepting tensors from any allocator.
 
 Blocks are pooled: when the last tensor over a block goes, the block returns
-to an idle list (keyed by size, at most `POOL_IDLE_BYTES` held) and the next
-request of that size reuses it without new mappings; `empty_cache()` releases
-the idle blocks.  Below `CHUNKED_MIN_BYTES` (data that fits the caches, and
-where mapping costs more than it saves) `share_block` is torch.empty.
+to an idle list (keyed by size) and the next request of that size reuses it
+without new mappings.  Reuse is stream-ordered, as in torch's caching
+allocator: a block remembers the stream it was allocated on (and any stream
+`record_stream` adds); when it goes idle an event is recorded on each of them
+(dn_block_record), and a request on stream S takes an idle block only when
+every such event is on S or has completed (dn_block_acquire) — the caller
+owns the shares it was handed (the reference's make_shares returns fresh
+objects, shamir.py:62-66), so no other stream's request gets them while that
+caller's work on them is still queued.  Only when a new block cannot be
+allocated does S wait (on the device, hipStreamWaitEvent) for a busy idle
+block instead.  A freed block waits for its own events, not the device.
+
+The pool holds at most `POOL_IDLE_BYTES`, and only while the device keeps
+`POOL_MIN_FREE` free beside them; before a new block is mapped, idle blocks
+(oldest first) are released until it fits with that headroom.  torch does
+not see this memory: `empty_cache()` releases the idle blocks (call it with
+torch.cuda.empty_cache()), and it runs by itself when torch reports an
+out-of-memory error, so the caller's retry finds the memory free.  Below
+`CHUNKED_MIN_BYTES` (data that fits the caches, and where mapping costs more
+than it saves) `share_block` is torch.empty.
 
 Chunked blocks are not always fast either (r04q: 2 of 12 at 0.66-0.67 of
 8 TB/s for the split, the rest 0.72-0.79), and a block's write rate predicts
@@ -23,7 +39,7 @@ profiles/r04/q/block_class.jsonl).  So a NEW share block of at least
 `PROBE_MIN_BYTES` is probed once (one timed write in the split's order:
 per tile, every row's slice) and kept only if it writes
 at >= `PROBE_KEEP` of the best rate this process has seen on the device
-for blocks of that many rows;
+for blocks of that many rows and that size class (log2 of the bytes);
 otherwise up to `PROBE_TRIES` blocks (at most `PROBE_BUDGET` bytes of them)
 are mapped and the fastest is kept (the others are freed after the choice, so
 a retry cannot get their pages back).
@@ -32,44 +48,71 @@ The first large block on a device is the faster of two.
 from __future__ import annotations
 
 import ctypes
+import itertools
 import math
 import threading
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 from . import _native
 
-__all__ = ["share_block", "chunked_block", "empty_cache", "granularity", "pool_stats", "block_rate"]
+__all__ = ["share_block", "chunked_block", "empty_cache", "granularity", "pool_stats", "block_rate",
+           "record_stream"]
 
 CHUNK_BYTES = 2 << 20          # physical chunk of a pooled block
 CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
-POOL_IDLE_BYTES = 64 << 30     # most idle bytes the pool keeps mapped
+POOL_IDLE_BYTES = 32 << 30     # most idle bytes the pool keeps mapped
+POOL_MIN_FREE = 16 << 30       # device bytes kept free beside the idle blocks
 PROBE_MIN_BYTES = 256 << 20    # new share blocks from this size up are write-rate probed
 PROBE_TRIES = 4                # most blocks mapped for one request
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
 PROBE_BUDGET = 24 << 30        # most bytes mapped at once for one request's tries
 
-_lock = threading.Lock()
-_idle: Dict[Tuple[int, int, int], List[int]] = {}  # (device, nbytes, chunk) -> idle block pointers
+_lock = threading.RLock()
+_idle: Dict[Tuple[int, int, int], List[Tuple[int, int]]] = {}  # (device, nbytes, chunk) -> [(age, ptr)]
 _idle_bytes = 0
-_stats = {"allocs": 0, "reuses": 0, "frees": 0, "probed": 0, "rejected": 0}
-_best_rate: Dict[Tuple[int, int], float] = {}  # (device, rows) -> fastest probed write rate (bytes/s)
+_age = itertools.count()
+_stats = {"allocs": 0, "reuses": 0, "frees": 0, "probed": 0, "rejected": 0, "waits": 0, "busy_skips": 0,
+          "trimmed": 0}
+_best_rate: Dict[Tuple[int, int, int], float] = {}  # (device, rows, log2 bytes) -> fastest probed write rate (B/s)
 _rates: Dict[int, float] = {}      # block pointer -> its probed write rate
+_live: Dict[int, "weakref.ref"] = {}  # block pointer -> its live _Block (record_stream)
+_observer = False
 
 
-def _free_ptr(ptr: int) -> None:
+def _raw_stream(stream) -> int:
+    if stream is None:
+        return 0
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+def _free_ptr(ptr: int, streams: Sequence[int] = ()) -> None:
+    """Free a block after its uses on `streams` (events recorded here) and the
+    ones recorded when it went idle (dn_block_free waits for them)."""
     _rates.pop(ptr, None)
+    L = _native.lib()
+    for s in streams:
+        _native.check(L.dn_block_record(ptr, s or None))
     _native.lib().dn_block_free(ptr)
     _stats["frees"] += 1
+
+
+def _mem_info(index: int) -> Tuple[int, int]:
+    import torch
+
+    return torch.cuda.mem_get_info(index)
 
 
 class _Block:
     """One dn_block_alloc block seen through __cuda_array_interface__ (v3).
     torch.as_tensor keeps this object alive as long as the tensor; when it
-    goes, the block returns to the idle pool (or is freed: pool full, or
-    pooled=False)."""
+    goes, events are recorded on the streams that used the block and the block
+    returns to the idle pool (or is freed: pool full, device short of memory,
+    or pooled=False)."""
 
-    def __init__(self, ptr: int, key: Tuple[int, int, int], shape, pooled: bool):
+    def __init__(self, ptr: int, key: Tuple[int, int, int], shape, pooled: bool, stream: int):
         self.ptr, self.key, self.pooled = ptr, key, pooled
+        self.streams = {stream}
         self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "|u1", "data": (ptr, False),
                                          "version": 3, "strides": None}
 
@@ -79,11 +122,16 @@ class _Block:
         if not ptr:
             return
         try:
+            _live.pop(ptr, None)
+            L = _native.lib()
+            for s in self.streams:
+                _native.check(L.dn_block_record(ptr, s or None))
             if self.pooled:
+                nbytes = self.key[1]
                 with _lock:
-                    if _idle_bytes + self.key[1] <= POOL_IDLE_BYTES:
-                        _idle.setdefault(self.key, []).append(ptr)
-                        _idle_bytes += self.key[1]
+                    if _idle_bytes + nbytes <= POOL_IDLE_BYTES and _mem_info(self.key[0])[0] >= POOL_MIN_FREE:
+                        _idle.setdefault(self.key, []).append((next(_age), ptr))
+                        _idle_bytes += nbytes
                         return
             _free_ptr(ptr)
         except Exception:  # interpreter shutdown: the process releases the memory
@@ -96,6 +144,72 @@ class _View:
     def __init__(self, ptr: int, nbytes: int):
         self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
                                          "version": 3, "strides": None}
+
+
+def _on_oom(*_args) -> None:
+    try:
+        empty_cache()
+    except Exception:
+        pass
+
+
+def _attach_oom_observer() -> None:
+    """torch's out-of-memory error releases the idle blocks (torch cannot see them)."""
+    global _observer
+    if _observer:
+        return
+    _observer = True
+    try:
+        import torch
+
+        torch._C._cuda_attach_out_of_memory_observer(_on_oom)
+    except Exception:  # an older torch: empty_cache() stays the caller's call
+        pass
+
+
+def _take_idle(key: Tuple[int, int, int], stream: int, wait: bool = False) -> Optional[int]:
+    """An idle block of `key` usable on `stream`: one whose recorded uses are
+    on `stream` or complete; with wait, any (the stream waits for its events)."""
+    global _idle_bytes
+    L = _native.lib()
+    with _lock:
+        lst = _idle.get(key)
+        if not lst:
+            return None
+        for i in range(len(lst) - 1, -1, -1):  # the most recently idled first
+            ptr = lst[i][1]
+            rc = L.dn_block_acquire(ptr, stream or None, 1 if wait else 0)
+            if rc == _native.DN_ERR_RETRY:
+                _stats["busy_skips"] += 1
+                continue
+            _native.check(rc)
+            lst.pop(i)
+            _idle_bytes -= key[1]
+            _stats["reuses"] += 1
+            _stats["waits"] += int(wait)
+            return ptr
+    return None
+
+
+def _trim_for(nbytes: int, index: int) -> None:
+    """Release idle blocks (oldest first) until `nbytes` more fit on the
+    device with POOL_MIN_FREE to spare."""
+    global _idle_bytes
+    with _lock:
+        if not _idle_bytes:
+            return
+        free = _mem_info(index)[0]
+        order = sorted((age, key, ptr) for key, lst in _idle.items() if key[0] == index for age, ptr in lst)
+        for age, key, ptr in order:
+            if free >= nbytes + POOL_MIN_FREE:
+                break
+            _idle[key].remove((age, ptr))
+            if not _idle[key]:
+                del _idle[key]
+            _idle_bytes -= key[1]
+            _free_ptr(ptr)
+            _stats["trimmed"] += 1
+            free += key[1]
 
 
 def _alloc_raw(nbytes: int, chunk_bytes: int, index: int) -> int:
@@ -147,7 +261,8 @@ def _write_rate(ptr: int, nbytes: int, dev, shape) -> float:
 
 def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
     """A new block, write-rate probed (see the module docstring)."""
-    kind = (dev.index, int(shape[0]) if len(shape) == 2 else 0)  # rates compare within one block shape class
+    # rates compare within one block class: row count and size (log2 of the bytes)
+    kind = (dev.index, int(shape[0]) if len(shape) == 2 else 0, max(1, nbytes).bit_length())
     best = _best_rate.get(kind)
     cands: List[Tuple[float, int]] = []
     tries = max(1, min(PROBE_TRIES, PROBE_BUDGET // max(1, nbytes)))
@@ -167,9 +282,10 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
         elif rate >= PROBE_KEEP * best:
             break
     rate, keep = max(cands)
+    stream = _current_stream(dev.index)  # the probe wrote the rejected blocks on this stream
     for r, p in cands:
         if p != keep:
-            _free_ptr(p)
+            _free_ptr(p, (stream,))
             _stats["rejected"] += 1
     _best_rate[kind] = max([best or 0.0] + [r for r, _ in cands])
     _rates[keep] = rate
@@ -196,36 +312,60 @@ def _device_index(device):
     return torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
 
 
+def _current_stream(index: int) -> int:
+    import torch
+
+    return int(torch._C._cuda_getCurrentRawStream(index))
+
+
 def chunked_block(shape: Union[int, Sequence[int]], chunk_bytes: int = CHUNK_BYTES, device=None,
                   pooled: bool = True, probe: bool = False):
     """uint8 device tensor of `shape` whose memory is `chunk_bytes` physical
     chunks mapped back to back (from the idle pool when one of this size is
-    there; probe: a new block is write-rate probed, see the module docstring)."""
-    global _idle_bytes
+    free for the current stream; probe: a new block is write-rate probed, see
+    the module docstring).  The block is recorded as used on the current
+    stream; `record_stream` adds others."""
     import torch
 
     dev = _device_index(device)
     shape = (int(shape),) if isinstance(shape, int) else tuple(int(s) for s in shape)
     nbytes = max(1, math.prod(shape))
     key = (dev.index, nbytes, int(chunk_bytes))
-    ptr = None
-    with _lock:
-        lst = _idle.get(key)
-        if lst:
-            ptr = lst.pop()
-            _idle_bytes -= nbytes
-            _stats["reuses"] += 1
+    stream = _current_stream(dev.index)
+    _attach_oom_observer()
+    ptr = _take_idle(key, stream)
     if ptr is None:
-        if probe and nbytes >= PROBE_MIN_BYTES:
-            ptr = _alloc_probed(nbytes, chunk_bytes, dev, shape)
-        else:
-            ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)
-    blk = _Block(ptr, key, shape, pooled)
+        _trim_for(nbytes, dev.index)
+        try:
+            if probe and nbytes >= PROBE_MIN_BYTES:
+                ptr = _alloc_probed(nbytes, chunk_bytes, dev, shape)
+            else:
+                ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)
+        except RuntimeError:
+            ptr = _take_idle(key, stream, wait=True)  # out of memory: order after a busy idle block's users
+            if ptr is None:
+                raise
+    blk = _Block(ptr, key, shape, pooled, stream)
     with torch.cuda.device(dev.index):
         t = torch.as_tensor(blk, device=dev)
     if t.data_ptr() != ptr or t.dtype != torch.uint8 or tuple(t.shape) != shape:
         raise RuntimeError("chunked_block: the tensor does not alias the block")
+    _live[ptr] = weakref.ref(blk)
     return t
+
+
+def record_stream(t, stream) -> None:
+    """Mark the pooled block under tensor `t` as used on `stream` (a
+    torch.cuda.Stream or a raw handle): when the block goes idle, requests on
+    other streams wait for the work queued on `stream` until then.  torch's
+    own Tensor.record_stream does nothing for memory torch did not allocate.
+    A tensor that is not over a pooled block is left alone."""
+    p = t.data_ptr()
+    for base, ref in list(_live.items()):
+        blk = ref()
+        if blk is not None and base <= p < base + blk.key[1]:
+            blk.streams.add(_raw_stream(stream))
+            return
 
 
 def share_block(shape: Union[int, Sequence[int]], device=None):
@@ -241,10 +381,11 @@ def share_block(shape: Union[int, Sequence[int]], device=None):
 
 
 def empty_cache() -> None:
-    """Release every idle pooled block (their memory returns to the device)."""
+    """Release every idle pooled block (their memory returns to the device,
+    each after the work recorded on it)."""
     global _idle_bytes
     with _lock:
-        ptrs = [p for lst in _idle.values() for p in lst]
+        ptrs = [p for lst in _idle.values() for _, p in lst]
         _idle.clear()
         _idle_bytes = 0
     for p in ptrs:

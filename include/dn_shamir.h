@@ -267,15 +267,30 @@ int dn_shamir_eval_at_host(const uint8_t* coeffs_be, const uint64_t* coeff_offse
  * the allocation granularity; 0 = 2 MiB) mapped back to back into one
  * reserved virtual range.  The split's rate depends on the physical pages of
  * its share block; this lets a caller choose the block's
- * composition.  dn_block_free synchronises the device, then unmaps and
- * releases every chunk; the block's virtual range stays reserved for the life
- * of the process (a new block mapped at a freed block's address had its bytes
- * change under later allocations: DESIGN.md §5.2).  Every other entry point
- * keeps taking caller-owned memory from any allocator.
+ * composition.  dn_block_free waits for the events the block's uses recorded
+ * (dn_block_record; a block with none recorded: everything queued on its own
+ * device), then unmaps and releases every chunk; the block's virtual range
+ * stays reserved for the life of the process (a new block mapped at a freed
+ * block's address had its bytes change under later allocations: DESIGN.md
+ * §5.2).  Every other entry point keeps taking caller-owned memory from any
+ * allocator.  The returned shares belong to the caller
+ * (delta_node/crypto/shamir/shamir.py:62-66), so a pooled block is handed to
+ * a new owner only once its last owner's work is ordered before the new
+ * owner's:
+ *   dn_block_record   record an event on `stream` for the block (call it for
+ *                     every stream that used the block, when the block goes idle)
+ *   dn_block_ready    *ready = 1 when every recorded event is on `stream` or
+ *                     has completed (the block may be used on `stream` now)
+ *   dn_block_acquire  hand the block to work on `stream`: wait = 0 fails with
+ *                     DN_ERR_RETRY while another stream's event is pending;
+ *                     wait = 1 makes `stream` wait for those events (no host wait)
  */
 int dn_block_granularity(int device, uint64_t* bytes);
 int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, void** ptr);
 int dn_block_free(void* ptr);
+int dn_block_record(void* ptr, void* stream);
+int dn_block_ready(void* ptr, void* stream, int* ready);
+int dn_block_acquire(void* ptr, void* stream, int wait);
 
 /*
  * Device, async on `stream`.  Zero `rows` rows of `row_bytes` (whole

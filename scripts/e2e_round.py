@@ -291,6 +291,8 @@ def main() -> int:
     ap.add_argument("--coeffs", choices=("prng", "mt"), default="prng")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--seal", action="store_true", help="send each body as the receiver's AES envelope (JSON form)")
+    ap.add_argument("--cold", action="store_true", help="no warm-up round: the first round of a fresh runner "
+                    "and peer (the peer is up and listening, nothing else)")
     args = ap.parse_args()
     if args.serve:
         serve(args.serve)
@@ -298,11 +300,13 @@ def main() -> int:
     proc = start_peer(args.port)
     try:
         _wait_ready(args.port)
-        run_round(1 << 12, args.port, coeffs=args.coeffs, seal=args.seal)  # warm-up: contexts, kernels, connections
+        if not args.cold:  # warm-up: contexts, kernels, connections
+            run_round(1 << 12, args.port, coeffs=args.coeffs, seal=args.seal)
         ok = True
         for r in range(args.rounds):
             st = run_round(1 << args.log2n, args.port, coeffs=args.coeffs, seed=r + 1, seal=args.seal)
-            st.update({"round": r, "N": 1 << args.log2n, "t": 3, "n": 5, "coeffs": args.coeffs, "sealed": args.seal})
+            st.update({"round": r, "N": 1 << args.log2n, "t": 3, "n": 5, "coeffs": args.coeffs, "sealed": args.seal,
+                       "cold": args.cold and r == 0})
             print(json.dumps(st), flush=True)
             ok = ok and st["peer_verified"]
     finally:

@@ -132,3 +132,177 @@ def test_share_block_write_rate_probe():
 def test_block_free_rejects_foreign_pointer():
     x = torch.empty(16, dtype=torch.uint8, device=dev())
     assert _native.lib().dn_block_free(x.data_ptr()) == _native.DN_ERR_ARG
+
+
+# ------------------------------------------------------------ stream-ordered reuse
+SLEEP_CYCLES = 200_000_000  # torch.cuda._sleep: keeps a stream busy for tens of ms or more
+
+
+def _ref_shares(seed, sec, t, n):
+    """make_shares_vec into torch.empty memory on the default stream."""
+    ref = shamir.SecretShare(t)
+    ref.random.seed(seed)
+    out = torch.empty((n, field.vec_bytes(sec.numel())), dtype=torch.uint8, device=dev())
+    ref.make_shares_vec(sec, n, out=out)
+    torch.cuda.synchronize()
+    return out
+
+
+def test_share_block_not_reused_while_another_stream_still_reads_it():
+    """The returned shares belong to the caller (shamir.py:62-66): a block
+    freed while stream A still has work queued on it is not handed to a
+    request on stream B — A's queued read sees A's shares, B gets its own."""
+    memory.empty_cache()
+    N = 1 << 18
+    sec_a = torch.randint(-(1 << 62), 1 << 62, (N,), dtype=torch.int64, device=dev())
+    sec_b = torch.randint(-(1 << 62), 1 << 62, (N,), dtype=torch.int64, device=dev())
+    want_a, want_b = _ref_shares(21, sec_a, 3, 5), _ref_shares(22, sec_b, 3, 5)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    a, b = shamir.SecretShare(3), shamir.SecretShare(3)
+    a.random.seed(21)
+    b.random.seed(22)
+    s0 = memory.pool_stats()
+    with torch.cuda.stream(sa):
+        out_a = a.make_shares_vec(sec_a, 5)  # a pooled block, used on stream A
+        ptr_a = out_a.data_ptr()
+        torch.cuda._sleep(SLEEP_CYCLES)
+        kept = out_a.clone()  # queued on A behind the sleep: reads the block later
+        del out_a
+        gc.collect()  # the block goes idle with A's read still queued
+    assert memory.pool_stats()["idle_blocks"] == s0["idle_blocks"] + 1
+    with torch.cuda.stream(sb):
+        out_b = b.make_shares_vec(sec_b, 5)  # same size, another stream
+    a_busy = not sa.query()
+    torch.cuda.synchronize()
+    assert a_busy, "stream A finished before the request on B: the test did not race"
+    assert out_b.data_ptr() != ptr_a
+    assert memory.pool_stats()["busy_skips"] > s0["busy_skips"]
+    assert torch.equal(kept, want_a) and torch.equal(out_b, want_b)
+    del out_b, kept
+    gc.collect()
+    memory.empty_cache()
+
+
+def test_share_block_reused_at_once_on_the_same_stream():
+    memory.empty_cache()
+    shape = (5, field.vec_bytes(1 << 18))
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x = memory.chunked_block(shape, device=dev())
+        ptr = x.data_ptr()
+        torch.cuda._sleep(SLEEP_CYCLES // 4)
+        x.fill_(1)
+        del x
+        gc.collect()
+        y = memory.chunked_block(shape, device=dev())  # stream order covers the queued fill
+        assert y.data_ptr() == ptr
+        y.fill_(2)
+    torch.cuda.synchronize()
+    assert int((y != 2).sum().item()) == 0
+    del y
+    gc.collect()
+    memory.empty_cache()
+
+
+def test_busy_idle_block_taken_with_a_device_wait():
+    """The out-of-memory fallback: a request on B takes a block A still uses,
+    and B waits for A's recorded event on the device (dn_block_acquire wait=1):
+    B's write lands after A's queued read."""
+    memory.empty_cache()
+    shape = (5, field.vec_bytes(1 << 18))
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(sa):
+        x = memory.chunked_block(shape, device=dev())
+        x.fill_(0x5A)
+        key = (dev().index, x.numel(), memory.CHUNK_BYTES)
+        torch.cuda._sleep(SLEEP_CYCLES)
+        kept = x.clone()
+        del x
+        gc.collect()
+    raw_b = sb.cuda_stream
+    assert memory._take_idle(key, raw_b) is None  # not ready for B
+    ptr = memory._take_idle(key, raw_b, wait=True)
+    assert ptr is not None
+    with torch.cuda.stream(sb):
+        blk = memory._Block(ptr, key, shape, True, raw_b)
+        y = torch.as_tensor(blk, device=dev())
+        y.fill_(0xC3)  # ordered after A's clone by the event wait
+    torch.cuda.synchronize()
+    assert int((kept != 0x5A).sum().item()) == 0 and int((y != 0xC3).sum().item()) == 0
+    del y, blk, kept
+    gc.collect()
+    memory.empty_cache()
+
+
+def test_record_stream_orders_reuse_after_a_second_stream():
+    memory.empty_cache()
+    shape = (5, field.vec_bytes(1 << 18))
+    sa, sc = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(sa):
+        x = memory.chunked_block(shape, device=dev())
+        x.fill_(0x11)
+        key = (dev().index, x.numel(), memory.CHUNK_BYTES)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sc):  # the caller hands the block to stream C
+        torch.cuda._sleep(SLEEP_CYCLES)
+        kept = x.clone()
+    memory.record_stream(x, sc)
+    del x
+    gc.collect()
+    assert memory._take_idle(key, sa.cuda_stream) is None  # C's queued read is pending
+    torch.cuda.synchronize()
+    p = memory._take_idle(key, sa.cuda_stream)
+    assert p is not None  # completed: free to take
+    memory._free_ptr(p)
+    assert int((kept != 0x11).sum().item()) == 0
+    memory.empty_cache()
+
+
+def test_make_shares_vec_t4_loop_on_a_side_stream_equals_host_draw():
+    """t = 4 takes the draw-then-split path: its coefficient block (pooled,
+    >= 64 MiB here) is dropped right after the split is queued, and every
+    iteration's output block goes back to the pool.  On a side stream, each
+    call equals the host draw + split of the same generator."""
+    memory.empty_cache()
+    N, t, n = 1 << 19, 4, 6
+    assert (t - 1) * field.vec_bytes(N) >= memory.CHUNKED_MIN_BYTES
+    sec = torch.randint(-(1 << 62), 1 << 62, (N,), dtype=torch.int64, device=dev())
+    a, ref = shamir.SecretShare(t), shamir.SecretShare(t)
+    a.random.seed(5)
+    ref.random.seed(5)
+    s = torch.cuda.Stream()
+    outs = []
+    s0 = memory.pool_stats()
+    with torch.cuda.stream(s):
+        for _ in range(4):
+            out = a.make_shares_vec(sec, n)
+            outs.append(out.clone())
+            del out
+            gc.collect()
+    torch.cuda.synchronize()
+    assert memory.pool_stats()["reuses"] > s0["reuses"]
+    for got in outs:
+        co = torch.from_numpy(_native.mt_draw_coeffs(ref.random, N, t - 1)).to(dev())
+        want = torch.empty_like(got)
+        _native.split_u64(sec, co, want, N, t, n)
+        assert torch.equal(got, want)
+    assert a.random.getstate() == ref.random.getstate()
+    memory.empty_cache()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two HIP devices")
+def test_block_free_waits_on_the_blocks_own_device():
+    """dn_block_free of a block on cuda:1 while cuda:0 is current: the wait is
+    on cuda:1's work (its recorded event), the free succeeds and cuda:0 stays
+    current."""
+    memory.empty_cache()
+    torch.cuda.set_device(0)
+    d1 = torch.device("cuda", 1)
+    x = memory.chunked_block((memory.CHUNKED_MIN_BYTES,), device=d1, pooled=False)
+    with torch.cuda.device(1):
+        torch.cuda._sleep(SLEEP_CYCLES // 4)
+        x.fill_(3)
+    del x
+    gc.collect()
+    assert torch.cuda.current_device() == 0
+    torch.cuda.synchronize(1)

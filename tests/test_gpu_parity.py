@@ -16,7 +16,7 @@ import pytest
 import torch
 
 from delta_node.crypto import shamir
-from delta_node.crypto.shamir import _native, field
+from delta_node.crypto.shamir import _native, field, memory
 from golden.fixtures import (P, chunk_digests, combine_digests, ints_to_limbs, limbs_to_ints, load_json, load_npz,
                              manifest, secrets_int64, unpack_share_bytes)
 from oracle import c_oracle
@@ -146,6 +146,16 @@ def test_split_2e24_digest_and_roundtrip():
     assert dig == d["digest"]
     N = d["N"]
     sec = torch.from_numpy(secrets_int64(d["secret_seed"], N)).to(dev())
+    # the path bench.py times (bench.py step()): the device MT draw into a
+    # share block (draw_coeffs_vec), then split_kernel<3> from those
+    # coefficients into a memory.share_block block — same reference digest
+    drawn = shamir.SecretShare(3)
+    drawn.random.seed(d["mt_seed"])
+    co = drawn.draw_coeffs_vec(N, dev())
+    blk = memory.share_block((5, field.vec_bytes(N)), dev())
+    _native.split_u64(sec, co, blk, N, 3, 5)
+    assert block_digest(blk, N) == d["digest"]
+    del co, blk
     ss = shamir.SecretShare(3)
     import itertools
 
@@ -397,6 +407,25 @@ def test_device_mt_draw_equals_host_draw_past_4096_substreams():
     b = random.Random()
     b.setstate(a.getstate())
     got = torch.empty((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    assert _native.mt_draw_coeffs_device(b, n, tm1, got)
+    want = torch.from_numpy(_native.mt_draw_coeffs(a, n, tm1)).to(dev())
+    assert torch.equal(got, want)
+    assert a.getstate() == b.getstate()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n,tm1", [((1 << 24) + 1, 1), ((1 << 23) + 1, 2)])
+def test_device_mt_draw_runtime_direct_level_even_last_row(n, tm1):
+    """Draws of 2^24-scale take ONE jump level through rows D_s computed on the
+    host at run time (csrc/host_gf2poly.cpp): the odd windows and the last one.
+    With n * tm1 = 2^24 + tm1 the draw has S = 1025 substreams, so the last
+    window (S - 1 = 1024) is EVEN — a row the odd-step recurrence does not
+    produce (the headline 2^24 x 2 draw ends on an odd one).  Byte-equal to the
+    sequential host draw, same final random.Random state."""
+    a = random.Random(n + tm1)
+    b = random.Random()
+    b.setstate(a.getstate())
+    got = torch.zeros((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
     assert _native.mt_draw_coeffs_device(b, n, tm1, got)
     want = torch.from_numpy(_native.mt_draw_coeffs(a, n, tm1)).to(dev())
     assert torch.equal(got, want)

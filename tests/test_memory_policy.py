@@ -27,7 +27,7 @@ class Fake:
     def rate(self, ptr, nbytes, dev, shape):
         return self.rate_of[ptr]
 
-    def free(self, ptr):
+    def free(self, ptr, streams=()):
         self.freed.append(ptr)
 
 
@@ -40,6 +40,7 @@ def fake(monkeypatch):
         monkeypatch.setattr(memory, "_free_ptr", f.free)
         monkeypatch.setattr(memory, "_best_rate", {})
         monkeypatch.setattr(memory, "_rates", {})
+        monkeypatch.setattr(memory, "_current_stream", lambda index: 0)
         return f
     return make
 
@@ -53,7 +54,7 @@ def test_first_block_is_the_faster_of_two(fake):
     f = fake([5.0, 7.0, 9.0])
     p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)
     assert f.rate_of[p] == 7.0 and f.freed == [0x1000] and f.rates == [9.0]
-    assert memory._best_rate[(0, 5)] == 7.0 and memory._rates[p] == 7.0
+    assert memory._best_rate[(0, 5, NB.bit_length())] == 7.0 and memory._rates[p] == 7.0
 
 
 def test_later_block_kept_when_close_to_the_best(fake):
@@ -76,7 +77,14 @@ def test_rates_compare_within_a_row_count(fake):
     f = fake([9.0, 9.5, 5.0, 5.1])
     memory._alloc_probed(NB, 2 << 20, DEV, (2, SHAPE[1]))  # coefficient-block class: best 9.5
     p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # share-block class starts fresh: best of two
-    assert f.rate_of[p] == 5.1 and memory._best_rate[(0, 5)] == 5.1
+    assert f.rate_of[p] == 5.1 and memory._best_rate[(0, 5, NB.bit_length())] == 5.1
+
+
+def test_rates_compare_within_a_size_class(fake):
+    f = fake([9.0, 9.5, 5.0, 5.1])
+    memory._alloc_probed(NB // 8, 2 << 20, DEV, (5, SHAPE[1] // 8))  # a small 5-row block: best 9.5
+    p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # a large one is its own class: best of two
+    assert f.rate_of[p] == 5.1 and f.rates == []
 
 
 def test_budget_limits_tries_for_huge_blocks(fake):
@@ -94,3 +102,126 @@ def test_out_of_memory_keeps_the_best_so_far(fake):
     with pytest.raises(RuntimeError):
         memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)
     assert g.freed == []
+
+
+# ---------------------------------------------------------------- the idle pool
+class FakeLib:
+    """dn_block_* with scripted stream events: `busy` holds the pointers whose
+    recorded uses on another stream have not completed."""
+
+    def __init__(self):
+        self.busy = set()
+        self.recorded = []
+        self.acquired = []
+        self.freed = []
+
+    def dn_block_record(self, ptr, stream):
+        self.recorded.append((ptr, stream or 0))
+        return 0
+
+    def dn_block_acquire(self, ptr, stream, wait):
+        if ptr in self.busy and not wait:
+            return memory._native.DN_ERR_RETRY
+        self.acquired.append((ptr, stream or 0, wait))
+        return 0
+
+    def dn_block_free(self, ptr):
+        self.freed.append(ptr)
+        return 0
+
+
+@pytest.fixture
+def pool(monkeypatch):
+    L = FakeLib()
+    state = {"free": 100 << 30}
+    monkeypatch.setattr(memory._native, "lib", lambda: L)
+    monkeypatch.setattr(memory, "_idle", {})
+    monkeypatch.setattr(memory, "_idle_bytes", 0)
+    monkeypatch.setattr(memory, "_rates", {})
+    monkeypatch.setattr(memory, "_live", {})
+    monkeypatch.setattr(memory, "_mem_info", lambda index: (state["free"], 288 << 30))
+    L.state = state
+    return L
+
+
+def idle(key, ptr):
+    """Put a block in the idle list as _Block.__del__ does."""
+    b = memory._Block(ptr, key, (key[1],), True, 7)
+    del b
+
+
+KEY = (0, 1 << 30, 2 << 20)
+
+
+def test_block_going_idle_records_every_stream_it_used(pool):
+    b = memory._Block(0x100, KEY, (KEY[1],), True, 7)
+    b.streams.add(9)
+    del b
+    assert sorted(pool.recorded) == [(0x100, 7), (0x100, 9)]
+    assert memory._idle[KEY] and memory._idle_bytes == KEY[1]
+
+
+def test_idle_block_reused_only_when_ready_for_the_stream(pool):
+    idle(KEY, 0x100)
+    pool.busy.add(0x100)  # another stream's work on it is still queued
+    assert memory._take_idle(KEY, 5) is None
+    assert memory._stats["busy_skips"] >= 1 and memory._idle_bytes == KEY[1]
+    pool.busy.clear()  # its event completed (or the request is on the same stream)
+    assert memory._take_idle(KEY, 5) == 0x100
+    assert pool.acquired[-1] == (0x100, 5, 0) and memory._idle_bytes == 0
+
+
+def test_busy_idle_block_taken_with_a_device_wait_only_on_request(pool):
+    idle(KEY, 0x100)
+    pool.busy.add(0x100)
+    assert memory._take_idle(KEY, 5, wait=True) == 0x100
+    assert pool.acquired[-1] == (0x100, 5, 1)
+
+
+def test_newest_ready_idle_block_first(pool):
+    idle(KEY, 0x100)
+    idle(KEY, 0x200)
+    pool.busy.add(0x200)
+    assert memory._take_idle(KEY, 5) == 0x100
+
+
+def test_block_not_pooled_when_the_device_is_short_of_memory(pool):
+    pool.state["free"] = memory.POOL_MIN_FREE - 1
+    idle(KEY, 0x100)
+    assert pool.freed == [0x100] and KEY not in memory._idle
+
+
+def test_idle_cap(pool, monkeypatch):
+    monkeypatch.setattr(memory, "POOL_IDLE_BYTES", 3 << 30)
+    for k in range(5):
+        idle(KEY, 0x100 * (k + 1))
+    assert len(memory._idle[KEY]) == 3 and pool.freed == [0x400, 0x500]
+
+
+def test_trim_releases_oldest_idle_blocks_until_the_new_block_fits(pool):
+    k2 = (0, 2 << 30, 2 << 20)
+    idle(KEY, 0x100)  # oldest
+    idle(k2, 0x200)
+    idle(KEY, 0x300)
+    pool.state["free"] = memory.POOL_MIN_FREE + (1 << 30)
+    memory._trim_for(3 << 30, 0)  # needs 2 GiB more: the two oldest go
+    assert pool.freed == [0x100, 0x200] and memory._idle == {KEY: [memory._idle[KEY][0]]}
+    assert memory._idle[KEY][0][1] == 0x300 and memory._idle_bytes == KEY[1]
+
+
+def test_empty_cache_releases_every_idle_block(pool):
+    idle(KEY, 0x100)
+    idle((0, 2 << 30, 2 << 20), 0x200)
+    memory.empty_cache()
+    assert sorted(pool.freed) == [0x100, 0x200] and memory._idle == {} and memory._idle_bytes == 0
+
+
+def test_record_stream_adds_a_stream_to_the_live_block(pool):
+    b = memory._Block(0x1000, KEY, (KEY[1],), True, 7)
+    memory._live[0x1000] = __import__("weakref").ref(b)
+    view = types.SimpleNamespace(data_ptr=lambda: 0x1000 + 4096)
+    memory.record_stream(view, types.SimpleNamespace(cuda_stream=11))
+    assert b.streams == {7, 11}
+    outside = types.SimpleNamespace(data_ptr=lambda: 0x1000 + KEY[1])
+    memory.record_stream(outside, 12)
+    assert b.streams == {7, 11}
