@@ -56,4 +56,8 @@ bool mt_final_state(const uint32_t* state, int idx, uint64_t words, uint32_t* fi
 // a row disagreed with the tabulated ones).
 constexpr uint64_t kMtRtRows = 2048;
 const uint64_t* mt_direct_rows_l14(uint64_t S, uint64_t* version);
+// D_1 .. D_nrows in sequence into out[nrows][kMtPolyWords] (the build's
+// generator of the embedded table, csrc/gen_mt_rt_rows.cpp); false: no
+// carry-less multiply, or a row disagreed with the tabulated ones.
+bool mt_rt_rows_compute(uint64_t* out, uint64_t nrows);
 }  // namespace dn

@@ -6,10 +6,19 @@
 // degree 19937; tools/gen_mt_jump.py).  For the largest draws it can take one
 // direct level instead of the radix-64 levels A then B if it has
 // D_s = x^(L - 624 + (s - 1) L) mod P for s up to ~2048 (L = 17 * 2^14): too
-// many rows to tabulate in source (5 MB), so they are computed here once per
-// process as D_{s+1} = D_s * x^L mod P from the tabulated D_1 and x^L = B_1,
-// one GF(2)[x] product and one Barrett reduction per row (carry-less
-// multiplies), and checked against the 63 tabulated direct rows D_2..D_64.
+// many rows to tabulate in source (5 MB), so they are computed here as
+// D_{s+1} = D_s * x^L mod P from the tabulated D_1 and x^L = B_1, one GF(2)[x]
+// product and one Barrett reduction per row (carry-less multiplies), and
+// checked against the 63 tabulated direct rows D_2..D_64.
+//
+// Computing the 1024 rows a 2^24 draw needs took ~0.13 s of a process's first
+// make_shares_vec, so the build computes all kMtRtRows
+// once (csrc/gen_mt_rt_rows.cpp -> lib/mt_rt_rows14.bin) and embeds them in
+// the library (csrc/mt_rt_rows14.S, .incbin); at first use the embedded rows
+// are checked — D_1..D_64 against the tabulated rows, and 16 rows spread over
+// the table against the recurrence D_s = D_{s-1} x^L — and used as they are.
+// A library built without the blob, or a blob that fails the check, falls
+// back to computing rows at run time.
 #include <immintrin.h>
 
 #include <cstdint>
@@ -130,10 +139,52 @@ bool set_row(Rows& R, uint64_t s, const uint64_t* prev, const uint64_t* mul) {
   return true;
 }
 
+// The embedded table (csrc/mt_rt_rows14.S): kMtRtRows rows, or none.
+extern "C" const uint64_t dn_mt_rt_rows14_blob[] __attribute__((weak, visibility("hidden")));
+extern "C" const uint64_t dn_mt_rt_rows14_blob_end[] __attribute__((weak, visibility("hidden")));
+
+// The embedded rows once checked (nullptr: absent or wrong).
+const uint64_t* embedded_rows() {
+  static const uint64_t* checked = [] () -> const uint64_t* {
+    const uint64_t* b = dn_mt_rt_rows14_blob;
+    if (!b || !dn_mt_rt_rows14_blob_end ||
+        static_cast<uint64_t>(dn_mt_rt_rows14_blob_end - b) != kMtRtRows * static_cast<uint64_t>(kW))
+      return nullptr;
+    for (int s = 1; s <= kMtDirectRows; ++s)
+      if (std::memcmp(b + (s - 1) * kW, kDirect14[s - 1], sizeof(uint64_t) * kW)) return nullptr;
+    Barrett br;
+    std::vector<uint64_t> r(kW);
+    for (uint64_t s = kMtRtRows; s > kMtRtRows - 16 * 127; s -= 127) {  // 16 rows, the last one included
+      br.mulmod(b + (s - 2) * kW, kJump14[kMtRowB + 1], r.data());
+      if (std::memcmp(r.data(), b + (s - 1) * kW, sizeof(uint64_t) * kW)) return nullptr;
+    }
+    return b;
+  }();
+  return checked;
+}
+
 }  // namespace
 
+bool mt_rt_rows_compute(uint64_t* out, uint64_t nrows) {
+  if (!__builtin_cpu_supports("pclmul") || nrows == 0) return false;
+  Barrett br;
+  std::memcpy(out, kDirect14[0], sizeof(uint64_t) * kW);  // D_1
+  for (uint64_t s = 2; s <= nrows; ++s) {
+    br.mulmod(out + (s - 2) * kW, kJump14[kMtRowB + 1], out + (s - 1) * kW);
+    if (s <= static_cast<uint64_t>(kMtDirectRows) &&
+        std::memcmp(out + (s - 1) * kW, kDirect14[s - 1], sizeof(uint64_t) * kW))
+      return false;
+  }
+  return true;
+}
+
 const uint64_t* mt_direct_rows_l14(uint64_t S, uint64_t* version) {
-  if (S < 2 || S - 1 > kMtRtRows || !__builtin_cpu_supports("pclmul")) return nullptr;
+  if (S < 2 || S - 1 > kMtRtRows) return nullptr;
+  if (const uint64_t* e = embedded_rows()) {
+    if (version) *version = ~0ull;  // every row, never changes
+    return e;
+  }
+  if (!__builtin_cpu_supports("pclmul")) return nullptr;
   Rows& R = rows14();
   std::lock_guard<std::mutex> g(R.m);
   if (!R.ok) return nullptr;

@@ -59,13 +59,14 @@ from . import _native
 __all__ = ["share_block", "chunked_block", "empty_cache", "granularity", "pool_stats", "block_rate",
            "record_stream"]
 
-CHUNK_BYTES = 2 << 20          # physical chunk of a pooled block
+CHUNK_BYTES = 16 << 20         # physical chunk of a pooled block
 CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
 POOL_IDLE_BYTES = 32 << 30     # most idle bytes the pool keeps mapped
 POOL_MIN_FREE = 16 << 30       # device bytes kept free beside the idle blocks
 PROBE_MIN_BYTES = 256 << 20    # new share blocks from this size up are write-rate probed
 PROBE_TRIES = 4                # most blocks mapped for one request
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
+PROBE_FAST = 6.5e12            # a tiled probe at this rate (B/s) keeps its block at once
 PROBE_BUDGET = 24 << 30        # most bytes mapped at once for one request's tries
 
 _lock = threading.RLock()
@@ -264,6 +265,9 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
     # rates compare within one block class: row count and size (log2 of the bytes)
     kind = (dev.index, int(shape[0]) if len(shape) == 2 else 0, max(1, nbytes).bit_length())
     best = _best_rate.get(kind)
+    from . import field
+
+    tiled = len(shape) == 2 and int(shape[0]) > 0 and int(shape[1]) % field.TILE_BYTES == 0
     cands: List[Tuple[float, int]] = []
     tries = max(1, min(PROBE_TRIES, PROBE_BUDGET // max(1, nbytes)))
     for k in range(tries):
@@ -276,8 +280,10 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
         rate = _write_rate(ptr, nbytes, dev, shape)
         _stats["probed"] += 1
         cands.append((rate, ptr))
+        if tiled and rate >= PROBE_FAST:  # in the fast class whatever came before
+            break
         if best is None:
-            if k >= 1:  # the first large block on this device: the faster of two
+            if k >= 1:  # the first large block of its class on this device: the faster of two
                 break
         elif rate >= PROBE_KEEP * best:
             break

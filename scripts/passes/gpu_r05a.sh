@@ -15,7 +15,7 @@ tail -1 $O/smoke.log
 echo "== pytest gpu" && timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 600 --timeout-method thread > $O/pytest_gpu.log 2>&1 || rc=$?
 tail -2 $O/pytest_gpu.log
 [ $rc -ne 0 ] && { echo "== rc $rc"; grep -E "FAILED|Error" $O/pytest_gpu.log | head -5; exit $rc; }
-echo "== vmm reuse probe (kernel modes)" && timeout -k 10 120 ./tools/vmm_reuse_probe 5 > $O/vmm_reuse_kernel.txt 2>&1 || rc=$?
+echo "== vmm reuse probe (kernel modes)" && timeout -k 10 120 ./tools/vmm_reuse_probe 7 > $O/vmm_reuse_kernel.txt 2>&1 || rc=$?
 grep "bad cycles" $O/vmm_reuse_kernel.txt
 [ $rc -ne 0 ] && { echo "== rc $rc"; tail -5 $O/vmm_reuse_kernel.txt; exit $rc; }
 echo "== bench" && timeout -k 10 700 python bench.py > $O/bench_n1.json 2> $O/bench_n1.err || rc=$?

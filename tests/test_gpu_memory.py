@@ -81,9 +81,12 @@ def test_make_shares_vec_default_output_is_share_block():
 
 def test_freed_block_address_is_never_reused():
     """A freed block's virtual range is retired (csrc/vmm_block.cpp): the next
-    block lands elsewhere, and its bytes stay put under later allocations.
-    (Before: a new block at a freed block's address had its contents change
-    under unrelated torch allocations — scripts/msv_block_debug.py, r04i.)"""
+    block lands elsewhere, its bytes stay put under later allocations, and the
+    torch segments allocated after the free keep theirs (no allocation gets a
+    freed block's pages under a live translation).  The cause, reproduced
+    without torch by tools/vmm_reuse_probe (modes 5/6, profiles/r05/vmm_reuse/):
+    a block mapped with fresh handles at a freed block's address is not the
+    memory the GPU accesses there — every word reads back wrong."""
     memory.empty_cache()
     shape = (5, field.vec_bytes(1 << 18))
     seen = set()
@@ -91,10 +94,11 @@ def test_freed_block_address_is_never_reused():
         b = memory.chunked_block(shape, device=dev(), pooled=False)
         assert b.data_ptr() not in seen
         seen.add(b.data_ptr())
-        b.fill_(0xA0 + k)
-        junk = [torch.full((shape[0] * shape[1],), 7, dtype=torch.uint8, device=dev()) for _ in range(3)]
+        junk = [torch.full((shape[0] * shape[1],), 7 + j, dtype=torch.uint8, device=dev()) for j in range(3)]
+        b.fill_(0xA0 + k)  # after torch's new segments: no torch allocation shares the block's pages
         torch.cuda.synchronize()
         assert int((b != 0xA0 + k).sum().item()) == 0
+        assert all(int((x != 7 + j).sum().item()) == 0 for j, x in enumerate(junk))
         del b, junk
         gc.collect()
     st = memory.pool_stats()
@@ -135,7 +139,20 @@ def test_block_free_rejects_foreign_pointer():
 
 
 # ------------------------------------------------------------ stream-ordered reuse
-SLEEP_CYCLES = 200_000_000  # torch.cuda._sleep: keeps a stream busy for tens of ms or more
+_cycles_per_ms = []
+
+
+def _busy(ms: float) -> None:
+    """Keep the current stream busy for about `ms` (torch.cuda._sleep,
+    calibrated once: its cycle count is a clock whose rate we do not assume)."""
+    if not _cycles_per_ms:
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        torch.cuda._sleep(10_000_000)
+        e.record()
+        e.synchronize()
+        _cycles_per_ms.append(10_000_000 / max(s.elapsed_time(e), 1e-3))
+    torch.cuda._sleep(int(ms * _cycles_per_ms[0]))
 
 
 def _ref_shares(seed, sec, t, n):
@@ -165,7 +182,7 @@ def test_share_block_not_reused_while_another_stream_still_reads_it():
     with torch.cuda.stream(sa):
         out_a = a.make_shares_vec(sec_a, 5)  # a pooled block, used on stream A
         ptr_a = out_a.data_ptr()
-        torch.cuda._sleep(SLEEP_CYCLES)
+        _busy(3000)
         kept = out_a.clone()  # queued on A behind the sleep: reads the block later
         del out_a
         gc.collect()  # the block goes idle with A's read still queued
@@ -190,7 +207,7 @@ def test_share_block_reused_at_once_on_the_same_stream():
     with torch.cuda.stream(s):
         x = memory.chunked_block(shape, device=dev())
         ptr = x.data_ptr()
-        torch.cuda._sleep(SLEEP_CYCLES // 4)
+        _busy(500)
         x.fill_(1)
         del x
         gc.collect()
@@ -215,7 +232,7 @@ def test_busy_idle_block_taken_with_a_device_wait():
         x = memory.chunked_block(shape, device=dev())
         x.fill_(0x5A)
         key = (dev().index, x.numel(), memory.CHUNK_BYTES)
-        torch.cuda._sleep(SLEEP_CYCLES)
+        _busy(3000)
         kept = x.clone()
         del x
         gc.collect()
@@ -244,7 +261,7 @@ def test_record_stream_orders_reuse_after_a_second_stream():
         key = (dev().index, x.numel(), memory.CHUNK_BYTES)
     torch.cuda.synchronize()
     with torch.cuda.stream(sc):  # the caller hands the block to stream C
-        torch.cuda._sleep(SLEEP_CYCLES)
+        _busy(3000)
         kept = x.clone()
     memory.record_stream(x, sc)
     del x
@@ -300,7 +317,7 @@ def test_block_free_waits_on_the_blocks_own_device():
     d1 = torch.device("cuda", 1)
     x = memory.chunked_block((memory.CHUNKED_MIN_BYTES,), device=d1, pooled=False)
     with torch.cuda.device(1):
-        torch.cuda._sleep(SLEEP_CYCLES // 4)
+        _busy(500)
         x.fill_(3)
     del x
     gc.collect()

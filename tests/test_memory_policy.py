@@ -57,6 +57,18 @@ def test_first_block_is_the_faster_of_two(fake):
     assert memory._best_rate[(0, 5, NB.bit_length())] == 7.0 and memory._rates[p] == 7.0
 
 
+def test_fast_class_block_kept_at_once(fake):
+    """A tiled (split-order) probe at >= PROBE_FAST keeps its block without
+    a second try, even as the first large block on the device."""
+    fast = memory.PROBE_FAST
+    f = fake([fast * 1.01, fast * 1.2])
+    p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)
+    assert f.rate_of[p] == fast * 1.01 and f.freed == [] and f.rates == [fast * 1.2]
+    g = fake([fast * 1.01, fast * 1.2])  # a linear-fill probe (untiled shape): the faster of two
+    q = memory._alloc_probed(NB, 2 << 20, DEV, (NB,))
+    assert g.rate_of[q] == fast * 1.2 and len(g.freed) == 1
+
+
 def test_later_block_kept_when_close_to_the_best(fake):
     f = fake([7.0, 6.0, 6.8])
     memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # best 7.0 (the first of two tries)
