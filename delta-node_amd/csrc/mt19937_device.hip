@@ -141,15 +141,6 @@ struct JumpJob {
 #define DN_MT_RT_DIRECT 1
 #endif
 
-// The runtime direct level in C chunks by substream range (build_levels):
-// chunk c's jumps, then the generation of its substreams on a stream of its
-// own, so the generation of the first substreams overlaps the later chunks'
-// jumps (DN_MT_RT_CHUNKS in the tuning build; 1: one level, one launch).
-#ifndef DN_MT_RT_CHUNKS
-#define DN_MT_RT_CHUNKS 1
-#endif
-constexpr int kMaxRtChunks = 4;  // the caller's stream, the jump stream and two more
-
 // A latency-bound level (few jobs: one Horner chain of ~312 steps per jump)
 // splits every jump into P parts over word ranges [lo, hi) of g.  Since
 // g(f) W = sum_k f^(64 k) g_k(f) W, part [lo, hi) evaluates
@@ -443,7 +434,6 @@ struct GenArgs {
   uint32_t ring;         // ring slots of one wave (2 emission groups; GenRing)
   uint32_t back;         // even substreams 2 .. S-2 run backward from the next window
   uint32_t probe;        // tuning build only (DN_MT_PROBE): 1 skip emissions, 2 skip generation
-  uint32_t sub0;         // substream of workgroup 0 (a launch over substreams sub0 ..)
 };
 
 // DN_MT_PROBE (tuning build): time the generation and the emission apart.
@@ -782,7 +772,7 @@ template <int T, int SAUX = kNt, int NS = 0>
 __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t sub = a.sub0 + blockIdx.x;
+  const uint32_t sub = blockIdx.x;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
   const bool fin_wave = sub == a.S;
   const bool fwd = fin_wave || mt_sub_forward(sub, a.S, static_cast<int>(a.back));
@@ -962,7 +952,7 @@ __global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const Ge
   const uint32_t lane = threadIdx.x & 63u;
   // (roles alternating with the workgroup's parity: no faster, profiles/r04/l/)
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 consumer, 1 producer
-  const uint32_t sub = a.sub0 + blockIdx.x;
+  const uint32_t sub = blockIdx.x;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
   const bool fin_wave = sub == a.S;
   const bool fwd = fin_wave || mt_sub_forward(sub, a.S, static_cast<int>(a.back));
@@ -1246,30 +1236,17 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
 // draws of up to kMtRtRows + 1 substreams of 2^14 draws that generate
 // backward: the 1024 windows of a 2^24-element 3-of-5 draw in one level of
 // ~150 us instead of level A (~28 us), its combine and level B (~148 us).
-// rt with chunks > 1: one level per substream range [bounds[c], bounds[c + 1])
-// (even bounds: a backward substream and the forward one after it share their
-// window, so the windows split with the ranges), levels that may run while
-// earlier chunks generate; their part rows are reused (one stream runs them).
-void build_levels(uint64_t S, int ki, int back, bool rt, int chunks, std::vector<Level>& lv,
-                  std::vector<uint32_t>& bounds) {
+void build_levels(uint64_t S, int ki, int back, bool rt, Level lv[3]) {
   const uint64_t R = kMtJumpRadix;
-  lv.assign(3, Level());
-  bounds.clear();
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
   const int32_t prow0 = static_cast<int32_t>(S + 1);
   if (rt) {
-    const int C = std::max(1, std::min(chunks, kMaxRtChunks));
-    if (C > 1) lv.assign(C, Level());
-    for (int c = 0; c <= C; ++c) bounds.push_back(c == C ? static_cast<uint32_t>(S) : static_cast<uint32_t>(S * c / C) & ~1u);
-    for (int c = 0; c < C; ++c) {
-      std::vector<std::pair<int32_t, int32_t>> pd;
-      for (uint64_t s = std::max<uint64_t>(1, bounds[c]); s < bounds[c + 1] || (c == C - 1 && s < S); ++s)
-        if (mt_window_needed(static_cast<uint32_t>(s), S, back))
-          pd.push_back({kMtRtBase + static_cast<int32_t>(s - 1), static_cast<int32_t>(s)});
-      push_level(lv[c], {{-1, pd}}, prow0);
-    }
-    if (C == 1) bounds.clear();
+    std::vector<std::pair<int32_t, int32_t>> pd;
+    for (uint64_t s = 1; s < S; ++s)
+      if (mt_window_needed(static_cast<uint32_t>(s), S, back))
+        pd.push_back({kMtRtBase + static_cast<int32_t>(s - 1), static_cast<int32_t>(s)});
+    push_level(lv[0], {{-1, pd}}, prow0);
     return;
   }
   if (last < static_cast<uint64_t>(kMtDirectRows)) {
@@ -1320,9 +1297,7 @@ struct MtHost {
   int back = 0;
   int parts_b = 0;  // tuning build: DN_MT_PARTS_B the levels were built with
   bool rt = false;  // one direct level through the runtime rows
-  int chunks = 1;   // rt: levels by substream range, each followed by its generation
-  std::vector<Level> lv;
-  std::vector<uint32_t> bounds;  // chunked rt: substream range of level c is [bounds[c], bounds[c + 1])
+  Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
 };
@@ -1350,10 +1325,9 @@ MtHost& mt_levels(uint64_t S, int ki) {
   const bool rt = DN_MT_RT_DIRECT && !(rte && rte[0] == '0') && ki == 2 && back == 1 &&
                   S - 1 > static_cast<uint64_t>(kMtDirectRows) && S - 1 <= kMtRtRows &&
                   mt_direct_rows_l14(S, nullptr) != nullptr;
-  const char* ce = tune_env("DN_MT_RT_CHUNKS");
-  const int chunks = rt ? (ce ? std::max(1, std::min(kMaxRtChunks, std::atoi(ce))) : DN_MT_RT_CHUNKS) : 1;
-  if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b || H.rt != rt || H.chunks != chunks) {
-    build_levels(S, ki, back, rt, chunks, H.lv, H.bounds);
+  if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b || H.rt != rt) {
+    for (auto& l : H.lv) l = Level();
+    build_levels(S, ki, back, rt, H.lv);
     uint64_t nj = 0, nc = 0;
     for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
     H.part_rows = 0;
@@ -1374,7 +1348,6 @@ MtHost& mt_levels(uint64_t S, int ki) {
     H.back = back;
     H.parts_b = parts_b;
     H.rt = rt;
-    H.chunks = chunks;
   }
   return H;
 }
@@ -1449,7 +1422,6 @@ struct DevJobs {
   uint64_t S;
   int ki, back, parts_b;
   bool rt;
-  int chunks;
   void* p;
 };
 
@@ -1463,8 +1435,7 @@ const void* device_jobs(const MtHost& H, int* err) {
   }
   std::lock_guard<std::mutex> g(*m);
   for (const DevJobs& d : *cache)
-    if (d.dev == dev && d.S == H.S && d.ki == H.ki && d.back == H.back && d.parts_b == H.parts_b && d.rt == H.rt &&
-        d.chunks == H.chunks)
+    if (d.dev == dev && d.S == H.S && d.ki == H.ki && d.back == H.back && d.parts_b == H.parts_b && d.rt == H.rt)
       return d.p;
   void* p = nullptr;
   const size_t bytes = std::max<size_t>(H.jobs.size() * 4, 16);
@@ -1474,7 +1445,7 @@ const void* device_jobs(const MtHost& H, int* err) {
     *err = 1;
     return nullptr;
   }
-  cache->push_back({dev, H.S, H.ki, H.back, H.parts_b, H.rt, H.chunks, p});
+  cache->push_back({dev, H.S, H.ki, H.back, H.parts_b, H.rt, p});
   return p;
 }
 
@@ -1521,39 +1492,6 @@ const uint64_t* device_rt(uint64_t S, int* err) {
     d->rows = n;
   }
   return d->p;
-}
-
-// The chunked runtime level's side streams and events, per thread and device
-// (created once, never destroyed: the runtime may go first).  Every call
-// synchronises the caller's stream, which waits for all of them, so a
-// thread's set is idle between its calls.
-struct MtStreams {
-  int dev;
-  hipStream_t j = nullptr;                      // the levels, then the last chunk's generation
-  hipStream_t g[kMaxRtChunks - 2] = {};         // middle chunks' generation
-  hipEvent_t start = nullptr;                   // the caller's copy done
-  hipEvent_t ready[kMaxRtChunks] = {};          // level c's windows done (on j)
-  hipEvent_t done[kMaxRtChunks] = {};           // a side stream's generation done
-};
-
-MtStreams* mt_streams(int C) {
-  thread_local std::vector<MtStreams>* all = new std::vector<MtStreams>;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  for (MtStreams& x : *all)
-    if (x.dev == dev) return &x;
-  MtStreams x;
-  x.dev = dev;
-  bool ok = hipStreamCreateWithFlags(&x.j, hipStreamNonBlocking) == hipSuccess &&
-            hipEventCreateWithFlags(&x.start, hipEventDisableTiming) == hipSuccess;
-  for (int k = 0; ok && k < kMaxRtChunks - 2; ++k) ok = hipStreamCreateWithFlags(&x.g[k], hipStreamNonBlocking) == hipSuccess;
-  for (int k = 0; ok && k < kMaxRtChunks; ++k)
-    ok = hipEventCreateWithFlags(&x.ready[k], hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&x.done[k], hipEventDisableTiming) == hipSuccess;
-  if (!ok) return nullptr;
-  (void)C;
-  all->push_back(x);
-  return &all->back();
 }
 
 // The call's end: DN_MT_SPIN_SYNC = 1 records an event behind the last
@@ -1640,12 +1578,8 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   // read back at the end.
   const int ki = mt_sub_len(ncoef);
   MtHost& H = mt_levels(S, ki);
-  const std::vector<Level>& lv = H.lv;
-  uint64_t njobs = 0;
-  for (const Level& l : lv) njobs += l.jobs.size();
-  const int C = static_cast<int>(H.bounds.size()) - 1;  // chunked levels (>= 2), or -1
-  MtStreams* xs = C >= 2 ? mt_streams(C) : nullptr;
-  if (C >= 2 && !xs) return set_error(DN_ERR_HIP, "%s: side streams", name);
+  const Level* lv = H.lv;
+  const uint64_t njobs = lv[0].jobs.size() + lv[1].jobs.size() + lv[2].jobs.size();
   int jerr = 0;
   const void* jobs_dev = device_jobs(H, &jerr);
   if (jerr) return set_error(DN_ERR_HIP, "%s: job tables on the device", name);
@@ -1669,44 +1603,23 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     (void)hipStreamSynchronize(s);  // the staging buffer is reused by the next call
     return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   }
-  // chunked: the levels run on the jump stream xs->j after the copy; level
-  // c's generation waits for its windows on a stream of its own (below)
-  hipStream_t js = s;
-  if (xs) {
-    err = hipEventRecord(xs->start, s);
-    if (err == hipSuccess) err = hipStreamWaitEvent(xs->j, xs->start, 0);
-    if (err != hipSuccess) {
-      (void)hipStreamSynchronize(s);
-      return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
-    }
-    js = xs->j;
-  }
-  std::vector<uint64_t> lv_off, lv_coff;  // each level's first job and combine job
-  {
-    uint64_t off = 0, coff = 0;
-    for (const Level& l : lv) {
-      lv_off.push_back(off);
-      lv_coff.push_back(coff);
-      off += l.jobs.size();
-      coff += l.comb.size();
-    }
-  }
-  auto launch_level = [&](int k, hipStream_t st) {
+  uint64_t off = 0, coff = 0;
+  for (int k = 0; k < 3; ++k) {
     const Level& l = lv[k];
     if (!l.jobs.empty()) {
       const char* jpr = tune_env("DN_MT_JUMP_PROBE");
-      const JumpArgs ja{dwin, djobs + lv_off[k], static_cast<uint32_t>(l.jobs.size()),
+      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.jobs.size()),
                         jpr ? static_cast<uint32_t>(std::atoi(jpr)) : 0u, rt_dev};
       const dim3 grid(static_cast<uint32_t>(l.jobs.size() / static_cast<size_t>(l.W)));
-      if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, st, ja);
-      else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, st, ja);
+      if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, s, ja);
+      else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, s, ja);
     }
     if (!l.comb.empty())
-      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(l.comb.size())), dim3(640), 0, st, dwin,
-                         dcomb + lv_coff[k]);
-  };
-  if (!xs)
-    for (int k = 0; k < static_cast<int>(lv.size()); ++k) launch_level(k, s);
+      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(l.comb.size())), dim3(640), 0, s, dwin,
+                         dcomb + coff);
+    off += l.jobs.size();
+    coff += l.comb.size();
+  }
   GenArgs ga{};
   ga.wins = dwin;
 #if DN_MT_HOST_HEAD
@@ -1736,34 +1649,8 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   ga.back = static_cast<uint32_t>(H.back);
   const char* pr = tune_env("DN_MT_PROBE");
   ga.probe = pr ? static_cast<uint32_t>(std::atoi(pr)) : 0u;
-  if (!xs) {
-    launch_gen(ga, s, S + 1);
-  } else {
-    // level c, then its substreams' generation: chunk 0 on the caller's
-    // stream, the middle ones on side streams, the last one (with the
-    // final-state workgroup) on the jump stream behind its own level; the
-    // caller's stream then waits for every side stream
-    for (int c = 0; c < C; ++c) {
-      launch_level(c, js);
-      GenArgs gc = ga;
-      gc.sub0 = H.bounds[c];
-      const uint32_t count = H.bounds[c + 1] - H.bounds[c] + (c == C - 1 ? 1u : 0u);
-      if (c == C - 1) {
-        launch_gen(gc, js, count);
-        break;
-      }
-      hipStream_t gs = c == 0 ? s : xs->g[c - 1];
-      if (hipEventRecord(xs->ready[c], js) != hipSuccess || hipStreamWaitEvent(gs, xs->ready[c], 0) != hipSuccess)
-        err = hipErrorUnknown;
-      launch_gen(gc, gs, count);
-    }
-    for (int c = 0; c < C - 1; ++c) {  // the caller's stream ends after all of them
-      hipStream_t side = c == 0 ? js : xs->g[c - 1];
-      if (hipEventRecord(xs->done[c], side) != hipSuccess || hipStreamWaitEvent(s, xs->done[c], 0) != hipSuccess)
-        err = hipErrorUnknown;
-    }
-  }
-  if (err == hipSuccess) err = hipGetLastError();
+  launch_gen(ga, s);
+  err = hipGetLastError();
   if (err != hipSuccess) {
     (void)hipStreamSynchronize(s);
     return set_error(DN_ERR_HIP, "%s: launch: %s", name, hipGetErrorString(err));
@@ -1795,7 +1682,7 @@ constexpr int kSc1 = DN_MT_SAUX;
 #endif  // buffer-store cache policy of the 3-of-5 share stores: sc1 (16)
 
 template <int T>
-void launch_gen(GenArgs& ga, hipStream_t s, uint32_t nblocks) {
+void launch_gen(GenArgs& ga, hipStream_t s) {
   ga.ring = 2u * 17u * 64u * (T ? T - 1 : 1);
   const uint32_t lds_words = 1u + ga.ring + 64u;  // GenRing: alignment word, ring, mirror
 #ifdef DN_TUNING
@@ -1804,7 +1691,7 @@ void launch_gen(GenArgs& ga, hipStream_t s, uint32_t nblocks) {
   if (sa && T == 3 && ga.n_shares == 5) {
     const int aux = std::atoi(sa);
     constexpr int NS = T == 3 ? 5 : 0;
-    const dim3 g(nblocks), b(64);
+    const dim3 g(ga.S + 1), b(64);
     if (aux == 0) hipLaunchKernelGGL((mt_gen_kernel<T, 0, NS>), g, b, lds_words * 4u, s, ga);
     else if (aux == 1) hipLaunchKernelGGL((mt_gen_kernel<T, 1, NS>), g, b, lds_words * 4u, s, ga);
     else if (aux == 2) hipLaunchKernelGGL((mt_gen_kernel<T, 2, NS>), g, b, lds_words * 4u, s, ga);
@@ -1826,17 +1713,17 @@ void launch_gen(GenArgs& ga, hipStream_t s, uint32_t nblocks) {
     const bool pc = !(pf && pf[0] == '0');
     if (pc) {
       if (T == 3 && ga.n_shares == 5)
-        hipLaunchKernelGGL((mt_gen_pc_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(nblocks), dim3(128), lds_words * 4u, s,
+        hipLaunchKernelGGL((mt_gen_pc_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(128), lds_words * 4u, s,
                            ga);
       else
-        hipLaunchKernelGGL((mt_gen_pc_kernel<T>), dim3(nblocks), dim3(128), lds_words * 4u, s, ga);
+        hipLaunchKernelGGL((mt_gen_pc_kernel<T>), dim3(ga.S + 1), dim3(128), lds_words * 4u, s, ga);
       return;
     }
   }
   if (T == 3 && ga.n_shares == 5)
-    hipLaunchKernelGGL((mt_gen_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(nblocks), dim3(64), lds_words * 4u, s, ga);
+    hipLaunchKernelGGL((mt_gen_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
   else
-    hipLaunchKernelGGL((mt_gen_kernel<T>), dim3(nblocks), dim3(64), lds_words * 4u, s, ga);
+    hipLaunchKernelGGL((mt_gen_kernel<T>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
 }
 
 }  // namespace
@@ -1846,9 +1733,9 @@ extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_ind
                                              void* coeffs, void* scratch, uint64_t scratch_bytes, void* stream) {
   if (n_elem && tm1 > 0 && !coeffs) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
   return mt_device_run("dn_mt19937_draw_coeffs_device", mt_state, mt_index, n_elem, tm1, scratch, scratch_bytes, stream,
-                       [&](GenArgs& ga, hipStream_t s, uint32_t nb) {
+                       [&](GenArgs& ga, hipStream_t s) {
                          ga.coeffs = static_cast<uint8_t*>(coeffs);
-                         launch_gen<0>(ga, s, nb);
+                         launch_gen<0>(ga, s);
                        });
 }
 
@@ -1873,12 +1760,12 @@ extern "C" int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, co
                      name, threshold, n_shares);
   if (n_elem && (!secrets || !shares)) return set_error(DN_ERR_ARG, "%s: null pointer", name);
   return mt_device_run(name, mt_state, mt_index, n_elem, threshold - 1, scratch, scratch_bytes, stream,
-                       [&](GenArgs& ga, hipStream_t s, uint32_t nb) {
+                       [&](GenArgs& ga, hipStream_t s) {
                          ga.secrets = secrets;
                          ga.shares = static_cast<uint8_t*>(shares);
                          ga.n_shares = n_shares;
-                         if (threshold == 2) launch_gen<2>(ga, s, nb);
-                         else if (threshold == 3) launch_gen<3>(ga, s, nb);
-                         else launch_gen<5>(ga, s, nb);
+                         if (threshold == 2) launch_gen<2>(ga, s);
+                         else if (threshold == 3) launch_gen<3>(ga, s);
+                         else launch_gen<5>(ga, s);
                        });
 }

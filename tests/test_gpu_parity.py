@@ -533,40 +533,6 @@ def test_fused_draw_split_declines_and_falls_back():
     assert ss.random.getstate() == ref.random.getstate()
 
 
-@pytest.mark.slow
-@pytest.mark.parametrize("chunks", [2, 3, 4])
-def test_runtime_level_in_chunks_equals_one_level(chunks, monkeypatch):
-    """The runtime direct level split by substream range (DN_MT_RT_CHUNKS,
-    tuning build: each chunk's jumps, then its substreams' generation on a
-    stream of its own while later chunks jump) computes exactly the one-level
-    draw: the fused 3-of-5 split of a ragged 2^23-scale vector (S = 1025
-    substreams, windows split over the chunks) and a 2^24 + 1 coefficient draw,
-    byte-equal blocks and equal final states."""
-    N = (1 << 23) + 12345
-    sec = torch.from_numpy(secrets_int64(chunks, N)).to(dev())
-    ref = shamir.SecretShare(3)
-    ref.random.seed(40 + chunks)
-    want = torch.zeros((5, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
-    assert _native.mt_split_device(ref.random, sec, want, N, 3, 5)
-    nd = (1 << 24) + 1
-    a = random.Random(50 + chunks)
-    b = random.Random()
-    b.setstate(a.getstate())
-    want_d = torch.zeros((1, field.vec_bytes(nd)), dtype=torch.uint8, device=dev())
-    assert _native.mt_draw_coeffs_device(a, nd, 1, want_d)
-    monkeypatch.setenv("DN_MT_RT_CHUNKS", str(chunks))
-    with _native.library(_native.TUNING_LIB):
-        ss = shamir.SecretShare(3)
-        ss.random.seed(40 + chunks)
-        got = torch.zeros_like(want)
-        assert _native.mt_split_device(ss.random, sec, got, N, 3, 5)
-        got_d = torch.zeros_like(want_d)
-        assert _native.mt_draw_coeffs_device(b, nd, 1, got_d)
-    torch.cuda.synchronize()
-    assert torch.equal(got, want) and ss.random.getstate() == ref.random.getstate()
-    assert torch.equal(got_d, want_d) and a.getstate() == b.getstate()
-
-
 def test_draw_coeffs_vec_device_path_matches_reference_fixture():
     """draw_coeffs_vec (device MT by default) reproduces the coefficients the
     reference consumed for F1 (tests/golden), and the split from them matches."""
