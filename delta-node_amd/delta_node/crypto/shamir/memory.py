@@ -63,7 +63,7 @@ CHUNK_BYTES = 16 << 20         # physical chunk of a pooled block
 CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
 POOL_IDLE_BYTES = 32 << 30     # most idle bytes the pool keeps mapped
 POOL_MIN_FREE = 16 << 30       # device bytes kept free beside the idle blocks
-PROBE_MIN_BYTES = 256 << 20    # new share blocks from this size up are write-rate probed
+PROBE_MIN_BYTES = 64 << 20     # new share blocks from this size up are write-rate probed (every chunked one)
 PROBE_TRIES = 4                # most blocks mapped for one request
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
 PROBE_FAST = 6.5e12            # a tiled probe at this rate (B/s) keeps its block at once

@@ -126,7 +126,7 @@ def test_share_block_write_rate_probe():
     c = memory.share_block((nb,), dev())  # the idle block comes back, no new probe
     assert c.data_ptr() == ptr and memory.pool_stats()["probed"] == st["probed"]
     assert memory.block_rate(c) is not None
-    small = memory.share_block((memory.CHUNKED_MIN_BYTES + 4096,), dev())  # below PROBE_MIN_BYTES: not probed
+    small = memory.share_block((memory.CHUNKED_MIN_BYTES - 4096,), dev())  # below CHUNKED_MIN_BYTES: torch.empty
     assert memory.block_rate(small) is None
     del c, small
     gc.collect()
