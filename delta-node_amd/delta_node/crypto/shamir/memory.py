@@ -64,7 +64,8 @@ CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
 POOL_IDLE_BYTES = 32 << 30     # most idle bytes the pool keeps mapped
 POOL_MIN_FREE = 16 << 30       # device bytes kept free beside the idle blocks
 PROBE_MIN_BYTES = 64 << 20     # new share blocks from this size up are write-rate probed (every chunked one)
-PROBE_TRIES = 4                # most blocks mapped for one request
+PROBE_TRIES = 4                # most blocks mapped for one request (blocks of 1 GiB or more)
+PROBE_TRIES_SMALL = 12         # ... for smaller blocks (a try maps a few chunks and writes for microseconds)
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
 PROBE_FAST = 6.5e12            # a tiled probe at this rate (B/s) keeps its block at once
 PROBE_BUDGET = 24 << 30        # most bytes mapped at once for one request's tries
@@ -269,7 +270,8 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
 
     tiled = len(shape) == 2 and int(shape[0]) > 0 and int(shape[1]) % field.TILE_BYTES == 0
     cands: List[Tuple[float, int]] = []
-    tries = max(1, min(PROBE_TRIES, PROBE_BUDGET // max(1, nbytes)))
+    most = PROBE_TRIES if nbytes >= (1 << 30) else PROBE_TRIES_SMALL
+    tries = max(1, min(most, PROBE_BUDGET // max(1, nbytes)))
     for k in range(tries):
         try:
             ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)

@@ -76,13 +76,25 @@ def test_later_block_kept_when_close_to_the_best(fake):
     assert f.rate_of[p] == 6.8 and f.rates == []
 
 
+BIG = (5, 16896 * 16384)  # 1.38 GB: a 2^22-element share block
+NBIG = BIG[0] * BIG[1]
+
+
 def test_slow_block_redrawn_up_to_the_try_limit(fake):
     f = fake([7.0, 6.0, 5.0, 5.5, 6.5, 5.2, 9.9])
-    memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # keeps 7.0, frees 6.0
-    p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # 5.0, 5.5, 6.5, 5.2: none close, keeps 6.5
+    memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # keeps 7.0, frees 6.0
+    p = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # 5.0, 5.5, 6.5, 5.2: none close, keeps 6.5
     assert f.rate_of[p] == 6.5
     assert sorted(f.rate_of[q] for q in f.freed) == [5.0, 5.2, 5.5, 6.0]
     assert f.rates == [9.9]  # PROBE_TRIES blocks at most
+
+
+def test_small_blocks_get_more_tries(fake):
+    rates = [7.0, 6.0] + [5.0] * (memory.PROBE_TRIES_SMALL - 1) + [6.9, 9.9]
+    f = fake(rates)
+    memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # keeps 7.0
+    p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # 11 slow tries, then 6.9 >= 0.96 * 7.0
+    assert f.rate_of[p] == 6.9 and f.rates == [9.9]
 
 
 def test_rates_compare_within_a_row_count(fake):
