@@ -1072,6 +1072,11 @@ def main():
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
 
+    # HIP events on the launch stream bracket every kernel of the timed steps:
+    # two per step (before the split, between split and reconstruct); the
+    # reconstruct of step i ends at step i + 1's first event (the last one at
+    # one more).  Each event record is a queue packet of its own (~4-5 us of
+    # stream time at 2^21, r05g), so no third per step.
     def step(i, ev=None):
         b = i % nbuf
         if ev:
@@ -1080,30 +1085,30 @@ def main():
         if ev:
             ev[1].record(stream)
         _native.reconstruct(row_sets[b], w, out_u64=rec, n=N)
-        if ev:
-            ev[2].record(stream)
 
     def timed_steps(fn, steps):
         for i in range(args.warmup):
             fn(i)
         barrier()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+        end = torch.cuda.Event(enable_timing=True)
         barrier()
         t0 = time.perf_counter()
         for i in range(steps):
             fn(i, evs[i])
+        end.record(stream)
         barrier()
         el = time.perf_counter() - t0
         if dist_on:
             tt = torch.tensor([el], dtype=torch.float64, device=cdev)
             torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
             el = float(tt.item())
-        return el, evs
+        return el, evs + [[end]]
 
     elapsed, evs = timed_steps(step, args.steps)
-    split_each = [e[0].elapsed_time(e[1]) for e in evs]
+    split_each = [evs[i][0].elapsed_time(evs[i][1]) for i in range(args.steps)]
     split_ms = float(np.mean(split_each))
-    recon_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    recon_ms = float(np.mean([evs[i][1].elapsed_time(evs[i + 1][0]) for i in range(args.steps)]))
     split_by_buf = [float(np.mean(split_each[b::nbuf])) for b in range(min(nbuf, args.steps))]
 
     # ---- parity of what was timed (cheap, size-independent + sampled) -----
