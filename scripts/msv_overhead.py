@@ -32,7 +32,26 @@ for lg in (8, 12, 16, 20, 24):
         ss.make_shares_vec(sec, 5, out=sh)
     torch.cuda.synchronize()
     out[f"2^{lg}"] = (time.perf_counter() - t0) / reps * 1e3
-print(json.dumps({"make_shares_vec_ms_per_call": out}))
+# the product default: out=None (each call's share block from memory.share_block;
+# the previous call's block returns to the pool when its tensor is dropped)
+dflt = {}
+for lg in (20, 24):
+    N = 1 << lg
+    sec = torch.randint(-(1 << 62), 1 << 62, (N,), dtype=torch.int64, device=dev)
+    ss = shamir.SecretShare(3)
+    ss.random.seed(lg)
+    for _ in range(3):
+        sh = ss.make_shares_vec(sec, 5)
+        del sh
+    torch.cuda.synchronize()
+    reps = 50 if lg < 24 else 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sh = ss.make_shares_vec(sec, 5)
+        del sh
+    torch.cuda.synchronize()
+    dflt[f"2^{lg}"] = (time.perf_counter() - t0) / reps * 1e3
+print(json.dumps({"make_shares_vec_ms_per_call": out, "make_shares_vec_default_out_ms_per_call": dflt}))
 
 # the same 2^12 call through the C-ABI directly (arguments prepared once):
 # the difference to make_shares_vec is the binding's Python time per call
