@@ -67,7 +67,7 @@ PROBE_MIN_BYTES = 64 << 20     # new share blocks from this size up are write-ra
 PROBE_TRIES = 4                # most blocks mapped for one request (blocks of 1 GiB or more)
 PROBE_TRIES_SMALL = 12         # ... for smaller blocks (a try maps a few chunks and writes for microseconds)
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
-PROBE_FAST = 6.5e12            # a tiled probe at this rate (B/s) keeps its block at once
+PROBE_FAST = 6.8e12            # the first block of a class keeps at once at this tiled-probe rate (B/s)
 PROBE_BUDGET = 24 << 30        # most bytes mapped at once for one request's tries
 
 _lock = threading.RLock()
@@ -282,7 +282,7 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
         rate = _write_rate(ptr, nbytes, dev, shape)
         _stats["probed"] += 1
         cands.append((rate, ptr))
-        if tiled and rate >= PROBE_FAST:  # in the fast class whatever came before
+        if best is None and tiled and rate >= PROBE_FAST:  # the class's first block, in the fast class
             break
         if best is None:
             if k >= 1:  # the first large block of its class on this device: the faster of two

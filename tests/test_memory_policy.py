@@ -58,12 +58,16 @@ def test_first_block_is_the_faster_of_two(fake):
 
 
 def test_fast_class_block_kept_at_once(fake):
-    """A tiled (split-order) probe at >= PROBE_FAST keeps its block without
-    a second try, even as the first large block on the device."""
+    """The first block of a class whose tiled (split-order) probe reaches
+    PROBE_FAST is kept without a second try; later blocks compare with the
+    best rate seen."""
     fast = memory.PROBE_FAST
-    f = fake([fast * 1.01, fast * 1.2])
+    f = fake([fast * 1.01, fast * 1.2, fast * 1.02, fast * 1.25])
     p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)
-    assert f.rate_of[p] == fast * 1.01 and f.freed == [] and f.rates == [fast * 1.2]
+    assert f.rate_of[p] == fast * 1.01 and f.freed == [] and f.rates == [fast * 1.2, fast * 1.02, fast * 1.25]
+    memory._best_rate[(0, 5, NB.bit_length())] = fast * 1.3  # a faster block was seen since
+    q = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # 1.2 and 1.02 fall short of 0.96 x 1.3; 1.25 passes
+    assert f.rate_of[q] == fast * 1.25 and f.rates == []
     g = fake([fast * 1.01, fast * 1.2])  # a linear-fill probe (untiled shape): the faster of two
     q = memory._alloc_probed(NB, 2 << 20, DEV, (NB,))
     assert g.rate_of[q] == fast * 1.2 and len(g.freed) == 1
