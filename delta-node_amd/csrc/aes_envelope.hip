@@ -45,6 +45,12 @@
 #ifndef DN_AES_SDWA
 #define DN_AES_SDWA 1
 #endif
+// DN_AES_HEX_LDS (default 1): the encrypt-to-hex kernel turns base64 sextets
+// into hex digit pairs by LDS lookups (hex_lds_word) instead of the SWAR
+// base64 + hex arithmetic; 0 builds the SWAR form (A/B baseline).
+#ifndef DN_AES_HEX_LDS
+#define DN_AES_HEX_LDS 1
+#endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
 #ifndef DN_AES_NB
@@ -424,6 +430,63 @@ __device__ __forceinline__ uint32_t hex_digits(uint32_t x) {
 
 __device__ __forceinline__ uint32_t hex_digit(uint32_t v) { return v < 10u ? 0x30u + v : 0x57u + v; }
 
+// ---- base64 + hex by LDS lookup (DN_AES_HEX_LDS) ---------------------------------
+// The hex digits of the base64 character of a sextet, as two tables in one
+// 256-B row per sextet (the AES tables' layout): words 0..31 hold the digit
+// pair in bytes 0-1, words 32..63 in bytes 2-3, each 32 times (lane l reads
+// replica l % 32: conflict-free).  The LDS byte address of sextet s, table t,
+// is s << 8 | (lane % 32) << 2 | t << 7: a sextet already at bits 8..13 of a
+// register is ONE full-rate v_bitop3 from its address.  Per 48-byte unit this
+// replaces ~45 VALU per 24-bit group (spread, class offsets, hex nibbles) by
+// about a dozen plus four lookups: the kernel is VALU-issue-bound with the LDS
+// ~half busy (profiles/r04/pmc/summary.json), so moving work to the LDS pays.
+struct HexLds {
+  uint32_t row[64][64];
+};
+
+__device__ __forceinline__ uint32_t b64_char(uint32_t s) {
+  return s < 26u ? 0x41u + s : s < 52u ? 0x61u + s - 26u : s < 62u ? 0x30u + s - 52u : s == 62u ? 0x2Bu : 0x2Fu;
+}
+
+__device__ void build_hex(HexLds& H, uint32_t TH) {
+  uint32_t* flat = &H.row[0][0];
+  for (uint32_t w = threadIdx.x; w < 64u * 64u; w += TH) {
+    const uint32_t c = b64_char(w >> 6), pair = hex_digit(c >> 4) | (hex_digit(c & 15u) << 8);
+    flat[w] = (w & 32u) ? pair << 16 : pair;
+  }
+}
+
+// the table word of a sextet held at bits 8..13 of v (higher and lower bits
+// ignored): address (v & 0x3F00) | lane bits by one v_bitop3
+template <int T>
+__device__ __forceinline__ uint32_t hex_lookup(const HexLds& H, uint32_t v, uint32_t lb) {
+  uint32_t a;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(a) : "v"(v), "s"(0x3F00u), "v"(lb));  // (v & m) | lb
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&H.row[0][0]) + a + 128 * T);
+}
+
+// 12 big-endian words (48 bytes) -> 32 hex words (64 base64 characters): sextet
+// j of a word triple (w0, w1, w2) is moved to bits 8..13 by one shift or
+// funnel shift (sextet 3 sits there already), looked up, and two lookups are
+// ORed into each output word (hex of characters 2i, 2i + 1)
+__device__ __forceinline__ void hex_lds_unit(const HexLds& H, const uint32_t W[12], uint32_t lb, uint32_t h[32]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t w0 = W[3 * q], w1 = W[3 * q + 1], w2 = W[3 * q + 2];
+    const uint32_t v[16] = {w0 >> 18, w0 >> 12, w0 >> 6, w0, w0 << 6, __builtin_amdgcn_alignbit(w0, w1, 20),
+                            w1 >> 14, w1 >> 8, w1 >> 2, w1 << 4, __builtin_amdgcn_alignbit(w1, w2, 22),
+                            w2 >> 16, w2 >> 10, w2 >> 4, w2 << 2, w2 << 8};
+    uint32_t x[16];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      x[j] = hex_lookup<0>(H, v[j], lb);
+      x[j + 1] = hex_lookup<1>(H, v[j + 1], lb);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[8 * q + i] = x[2 * i] | x[2 * i + 1];
+  }
+}
+
 // 4 characters -> 8 hex digits (2 words, each character's high digit first)
 __device__ __forceinline__ void hex_word(uint32_t c, uint32_t& h0, uint32_t& h1) {
   const uint32_t hi = (c >> 4) & 0x0F0F0F0Fu, lo = c & 0x0F0F0F0Fu;
@@ -578,6 +641,16 @@ __device__ void encrypt_unit_slow(const AesLds<NTAB>& L, const uint32_t lw[2], c
 template <int NR, int NTAB, bool HEX>
 __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const AesArgs a) {
   DN_AES_PROLOGUE;
+#if DN_AES_HEX_LDS
+  constexpr bool kHexLds = HEX && NTAB == 4;
+  __shared__ HexLds HX;
+  if constexpr (kHexLds) {
+    build_hex(HX, TH);
+    __syncthreads();
+  }
+#else
+  constexpr bool kHexLds = false;
+#endif
   const uint64_t m = a.n + 16;
   // plaintext of blocks 3g-1 .. 3g+1 of the next whole unit, loaded before this unit's stores
   uint32_t R[16];
@@ -617,6 +690,16 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
         for (int i = 0; i < 4; ++i) W[4 * j + i] = __builtin_bswap32(W[4 * j + i]) ^ ks[i];
       }
     }
+#if DN_AES_HEX_LDS
+    if constexpr (kHexLds) {
+      uint32_t h[32];
+      hex_lds_unit(HX, W, lb, h);
+      uint8_t* o = a.out + 128 * g;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) store4(o + 16 * v, h[4 * v], h[4 * v + 1], h[4 * v + 2], h[4 * v + 3], a.plain != 0u);
+      continue;
+    }
+#endif
     uint32_t C[16];
     b64_unit(W, C);
     if constexpr (HEX) {
