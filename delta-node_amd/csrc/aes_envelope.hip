@@ -51,6 +51,13 @@
 #ifndef DN_AES_HEX_LDS
 #define DN_AES_HEX_LDS 1
 #endif
+// DN_AES_HEX_COAL (default 1, with DN_AES_HEX_LDS): a wave whose 64 lanes all
+// hold whole units stores its 8 KB of hex text line by line (hex_coalesce:
+// cross-lane transpose, each store instruction one contiguous KB) instead of
+// each lane its own 128 bytes (16 B in each of 64 lines per instruction).
+#ifndef DN_AES_HEX_COAL
+#define DN_AES_HEX_COAL 1
+#endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
 #ifndef DN_AES_NB
@@ -465,6 +472,43 @@ __device__ __forceinline__ uint32_t hex_lookup(const HexLds& H, uint32_t v, uint
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&H.row[0][0]) + a + 128 * T);
 }
 
+// The wave's 64 x 8 16-byte chunks (lane s holds the 128 text bytes of unit
+// g0 + s, chunk c = h[4c .. 4c + 3]) transposed so that chunk register v of
+// lane l is chunk l >> 3 of lane 8 v + (l & 7): store v then writes the
+// contiguous KB [1024 v, 1024 v + 1024) of the wave's text.  Three butterfly
+// stages each swap one lane bit with one chunk-index bit: lane bit 5 <-> bit 2
+// (v_permlane32_swap), 4 <-> 1 (v_permlane16_swap), 3 <-> 0 (a DPP row
+// rotation by 8 and selects).  All 64 lanes must be active.
+__device__ __forceinline__ void hex_coalesce(uint32_t h[32], uint32_t lane) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const auto r = __builtin_amdgcn_permlane32_swap(h[4 * c + w], h[4 * (c + 4) + w], false, false);
+      h[4 * c + w] = r[0];
+      h[4 * (c + 4) + w] = r[1];
+    }
+#pragma unroll
+  for (int c : {0, 1, 4, 5})
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const auto r = __builtin_amdgcn_permlane16_swap(h[4 * c + w], h[4 * (c + 2) + w], false, false);
+      h[4 * c + w] = r[0];
+      h[4 * (c + 2) + w] = r[1];
+    }
+  const bool b3 = (lane & 8u) != 0u;
+#pragma unroll
+  for (int c : {0, 2, 4, 6})
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t A = h[4 * c + w], B = h[4 * (c + 1) + w];
+      const uint32_t x = b3 ? A : B;
+      const uint32_t y = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, false));
+      h[4 * c + w] = b3 ? y : A;
+      h[4 * (c + 1) + w] = b3 ? B : y;
+    }
+}
+
 // 12 big-endian words (48 bytes) -> 32 hex words (64 base64 characters): sextet
 // j of a word triple (w0, w1, w2) is moved to bits 8..13 by one shift or
 // funnel shift (sextet 3 sits there already), looked up, and two lookups are
@@ -694,6 +738,17 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
     if constexpr (kHexLds) {
       uint32_t h[32];
       hex_lds_unit(HX, W, lb, h);
+#if DN_AES_HEX_COAL
+      if (__ballot(1) == ~0ull) {  // all 64 lanes here, each with a whole unit (units g0 .. g0 + 63)
+        const uint32_t lane = threadIdx.x & 63u;
+        hex_coalesce(h, lane);
+        uint8_t* o = a.out + 128 * (g - lane) + 128 * (lane & 7u) + 16 * (lane >> 3);
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+          store4(o + 1024 * v, h[4 * v], h[4 * v + 1], h[4 * v + 2], h[4 * v + 3], a.plain != 0u);
+        continue;
+      }
+#endif
       uint8_t* o = a.out + 128 * g;
 #pragma unroll
       for (int v = 0; v < 8; ++v) store4(o + 16 * v, h[4 * v], h[4 * v + 1], h[4 * v + 2], h[4 * v + 3], a.plain != 0u);

@@ -26,7 +26,7 @@ pytestmark = pytest.mark.gpu
 KEYS = [bytes(range(32)), bytes(range(100, 116)), bytes(range(7, 31))]
 NONCES = [bytes(16), b"\xff" * 16, b"\xff" * 15 + b"\xfd", bytes(8) + b"\xff" * 8, bytes(range(200, 216))]
 SIZES = [0, 1, 2, 15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 79, 80, 81, 95, 96, 97, 127, 128, 129,
-         191, 192, 1000, 3071, 3072, 3073, 12345]
+         191, 192, 1000, 3071, 3072, 3073, 6128, 6129, 12345, 98288]
 
 
 def dev():
