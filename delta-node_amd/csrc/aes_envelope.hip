@@ -58,6 +58,11 @@
 #ifndef DN_AES_HEX_COAL
 #define DN_AES_HEX_COAL 1
 #endif
+// DN_AES_PIPE (default 1): the three blocks of an encrypt unit software-
+// pipelined round by round (aes3_pipe) instead of all lookups then all XORs.
+#ifndef DN_AES_PIPE
+#define DN_AES_PIPE 1
+#endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
 #ifndef DN_AES_NB
@@ -182,17 +187,15 @@ __device__ __forceinline__ void addr_byte(uint32_t& ar, uint32_t s) {
 }
 
 // a ^ b ^ c in one v_bitop3 (table 0x96); the compiler leaves the round's
-// five-term XORs as four v_xor_b32.  xor3s takes a wave-uniform third operand
-// (a round-key SGPR: VOP3 reads at most one SGPR).
+// five-term XORs as four v_xor_b32 otherwise.  xor3s takes a wave-uniform
+// third operand (a round key).  The builtin, not inline asm: the compiler
+// then knows the instruction and schedules around it (inline asm blocks got
+// an s_nop between dependent ones).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 __device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
-  return r;
+  return __builtin_amdgcn_bitop3_b32(a, b, k, 0x96);
 }
 
 template <int K, int T>
@@ -318,6 +321,60 @@ __device__ __forceinline__ void aes_blocks(const AesLds<4>& L, const uint32_t lw
 #pragma unroll
   for (int b = 0; b < NB; ++b) aes_block<NR>(L, lw, a, s[b]);
 #endif
+}
+
+// Three blocks software-pipelined: block b's round r XORs (and its round r + 1
+// lookups) run while the other two blocks' lookups are in flight, instead of
+// all 48 lookups of a round, a wait for all of them, then all XORs (a wave
+// then has nothing for the LDS while it XORs, and its 4-bit lgkmcnt cannot
+// wait for only the oldest of 48 reads).  Each block's state still finishes a
+// round before its next lookups, in program order: A r, B r, C r, A r + 1, ...
+// The last lookups of each block are its final round's (same table reads).
+template <int NR>
+__device__ __forceinline__ void aes3_pipe(const AesLds<4>& L, const uint32_t lw[2], const AesArgs& a, uint32_t s[3][4]) {
+  uint32_t st[3][4];
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[b][i] = s[b][i] ^ a.rk[i];
+  uint32_t ar[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ar[c][t] = lw[t >> 1];
+  uint32_t x[3][4][4];
+  auto issue = [&](int b) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      x[b][c][0] = te_sdwa<3, 0>(L, st[b][c], ar[c][0]);
+      x[b][c][1] = te_sdwa<2, 1>(L, st[b][(c + 1) & 3], ar[c][1]);
+      x[b][c][2] = te_sdwa<1, 2>(L, st[b][(c + 2) & 3], ar[c][2]);
+      x[b][c][3] = te_sdwa<0, 3>(L, st[b][(c + 3) & 3], ar[c][3]);
+    }
+  };
+  auto mix = [&](int b, int r) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) st[b][c] = xor3s(xor3(x[b][c][0], x[b][c][1], x[b][c][2]), x[b][c][3], a.rk[4 * r + c]);
+  };
+  issue(0);
+  issue(1);
+  issue(2);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = 1; r < NR; ++r) {
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      mix(b, r);
+      issue(b);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      s[b][c] = xor3s(__builtin_amdgcn_perm(x[b][c][0], x[b][c][1], 0x06010C0Cu),
+                      __builtin_amdgcn_perm(x[b][c][2], x[b][c][3], 0x0C0C0402u), a.rk[4 * NR + c]);
 }
 
 // Counter block iv + b (mod 2^128) as big-endian words.
@@ -467,8 +524,7 @@ __device__ void build_hex(HexLds& H, uint32_t TH) {
 // ignored): address (v & 0x3F00) | lane bits by one v_bitop3
 template <int T>
 __device__ __forceinline__ uint32_t hex_lookup(const HexLds& H, uint32_t v, uint32_t lb) {
-  uint32_t a;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(a) : "v"(v), "s"(0x3F00u), "v"(lb));  // (v & m) | lb
+  const uint32_t a = __builtin_amdgcn_bitop3_b32(v, 0x3F00u, lb, 0xea);  // (v & m) | lb
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&H.row[0][0]) + a + 128 * T);
 }
 
@@ -542,9 +598,8 @@ __device__ __forceinline__ void hex_word(uint32_t c, uint32_t& h0, uint32_t& h1)
 // every high nibble is 2..7, a decimal digit, so only the low nibbles take
 // the letter test
 __device__ __forceinline__ void hex_word_b64(uint32_t c, uint32_t& h0, uint32_t& h1) {
-  uint32_t hi;
-  // (c >> 4) & 0x0F0F0F0F | 0x30303030 in one v_bitop3 ((S0 & S1) | S2: table 0xea; one SGPR operand)
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(hi) : "v"(c >> 4), "s"(0x0F0F0F0Fu), "v"(0x30303030u));
+  // (c >> 4) & 0x0F0F0F0F | 0x30303030 in one v_bitop3 ((S0 & S1) | S2: table 0xea)
+  const uint32_t hi = __builtin_amdgcn_bitop3_b32(c >> 4, 0x0F0F0F0Fu, 0x30303030u, 0xea);
   const uint32_t lo = hex_digits(c & 0x0F0F0F0Fu);
   h0 = __builtin_amdgcn_perm(hi, lo, 0x01050004u);
   h1 = __builtin_amdgcn_perm(hi, lo, 0x03070206u);
@@ -714,7 +769,9 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
       uint32_t ks[3][4];
 #pragma unroll
       for (int j = 0; j < 3; ++j) ctr_block(a.iv, 3 * g - 1 + j, ks[j]);
-      if constexpr (DN_AES_NB == 3) {
+      if constexpr (DN_AES_NB == 3 && DN_AES_PIPE && DN_AES_SDWA) {
+        aes3_pipe<NR>(L, lw, a, ks);
+      } else if constexpr (DN_AES_NB == 3) {
         aes_blocks<NR, 3>(L, lw, a, ks);
       } else {
         aes_blocks<NR, 2>(L, lw, a, ks);
