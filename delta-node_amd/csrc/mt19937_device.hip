@@ -215,7 +215,10 @@ constexpr int kJumpWaves = 16;  // at most this many jumps (waves) per workgroup
 constexpr int kMaxParts = DN_MT_MAX_PARTS;  // at most this many parts per jump
 
 // a ^ b ^ c in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96;
-// hipcc keeps two v_xor_b32 otherwise)
+// hipcc keeps two v_xor_b32 otherwise).  Inline asm on purpose in the jump
+// kernel's Horner step: with the compiler builtin the scheduler hoists the
+// table reads further and the kernel spills ~1,300 scratch accesses (the
+// generation kernels' bitop3 below are builtins: no spill there, fewer s_nop).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t d;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
@@ -484,12 +487,10 @@ __device__ __forceinline__ uint32_t ring_wrap(uint32_t s, uint32_t M) { return s
 // mt_mix in five VALU: y = bfi(UP, a, b); m ^ (y >> 1) ^ (-(b & 1) & A), the
 // last two terms by v_bitop3 ((S0 & S1) ^ S2, table 0x6a; S0 the index MSB).
 __device__ __forceinline__ uint32_t mt_mix5(uint32_t a, uint32_t b, uint32_t m) {
-  uint32_t y, r;
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(y) : "s"(kMtUp), "v"(a), "v"(b));
+  const uint32_t y = (kMtUp & a) | (~kMtUp & b);  // v_bfi_b32
   const uint32_t u = (y >> 1) ^ m;
   const uint32_t mk = static_cast<uint32_t>(static_cast<int32_t>(b << 31) >> 31);
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(r) : "v"(mk), "s"(kMtA), "v"(u));
-  return r;
+  return __builtin_amdgcn_bitop3_b32(mk, kMtA, u, 0x6a);  // (mk & A) ^ u
 }
 
 // B appends (B <= 3: the appends of a batch read no word another one of the
@@ -587,9 +588,8 @@ __device__ __forceinline__ void ring_init(uint32_t* Rg, const GenRing& g, const 
 __device__ __forceinline__ uint32_t mt_unmix(uint32_t x396, uint32_t x397, uint32_t x623, uint32_t x624) {
   const uint32_t t1 = x624 ^ x397, t0 = x623 ^ x396;
   const uint32_t m0 = static_cast<uint32_t>(static_cast<int32_t>(t0) >> 31);
-  uint32_t u0, up;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(u0) : "v"(m0), "s"(kMtA), "v"(t0));  // (m0 & A) ^ t0
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(up) : "s"(0x40000000u), "v"(t1), "v"(u0));
+  const uint32_t u0 = __builtin_amdgcn_bitop3_b32(m0, kMtA, t0, 0x6a);  // (m0 & A) ^ t0
+  const uint32_t up = (0x40000000u & t1) | (~0x40000000u & u0);        // v_bfi_b32
   return __builtin_amdgcn_alignbit(up, t0, 31);
 }
 
