@@ -737,6 +737,29 @@ __device__ void encrypt_unit_slow(const AesLds<NTAB>& L, const uint32_t lw[2], c
   }
 }
 
+// The plaintext of unit g (blocks 3g - 1 .. 3g + 1) into R.  The tuning
+// diagnostic DN_AES_DIAG_COAL_IN loads the same amount with the wave's
+// lanes contiguous (wrong bytes, timing only: is the strided load a cost?).
+__device__ __forceinline__ void load_unit(const AesArgs& a, uint64_t g, uint32_t (&R)[16]) {
+#ifdef DN_AES_DIAG_COAL_IN
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t w0 = 48 * (g - lane);
+  if (g < lane || w0 + 3072 > a.n) {  // the wave's window not wholly inside the message
+    load_raw<3>(a.in, a.skew, 48 * g - 16, R);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    uint32_t r[8];
+    load_raw<1>(a.in, 0u, w0 + 1024 * k + 16 * lane, r);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) R[4 * k + i] = r[i];
+  }
+#else
+  load_raw<3>(a.in, a.skew, 48 * g - 16, R);
+#endif
+}
+
 template <int NR, int NTAB, bool HEX>
 __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const AesArgs a) {
   DN_AES_PROLOGUE;
@@ -753,18 +776,18 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
   const uint64_t m = a.n + 16;
   // plaintext of blocks 3g-1 .. 3g+1 of the next whole unit, loaded before this unit's stores
   uint32_t R[16];
-  if (first < a.units && first != 0 && 48 * (first + 1) <= m) load_raw<3>(a.in, a.skew, 48 * first - 16, R);
+  if (first < a.units && first != 0 && 48 * (first + 1) <= m) load_unit(a, first, R);
   for (uint64_t g = first; g < a.units; g += stride) {
     const uint64_t gn = g + stride;
     const bool next_whole = gn < a.units && 48 * (gn + 1) <= m;
     if (g == 0 || 48 * (g + 1) > m) {
       encrypt_unit_slow<NR, NTAB, HEX>(L, lw, a, g);
-      if (next_whole) load_raw<3>(a.in, a.skew, 48 * gn - 16, R);
+      if (next_whole) load_unit(a, gn, R);
       continue;
     }
     uint32_t W[12];
     shift_raw<3>(R, a.skew, W);
-    if (next_whole) load_raw<3>(a.in, a.skew, 48 * gn - 16, R);
+    if (next_whole) load_unit(a, gn, R);
     if constexpr (NTAB == 4 && DN_AES_NB > 1) {
       uint32_t ks[3][4];
 #pragma unroll
