@@ -58,11 +58,6 @@
 #ifndef DN_AES_HEX_COAL
 #define DN_AES_HEX_COAL 1
 #endif
-// DN_AES_PIPE (default 1): the three blocks of an encrypt unit software-
-// pipelined round by round (aes3_pipe) instead of all lookups then all XORs.
-#ifndef DN_AES_PIPE
-#define DN_AES_PIPE 1
-#endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
 #ifndef DN_AES_NB
@@ -321,60 +316,6 @@ __device__ __forceinline__ void aes_blocks(const AesLds<4>& L, const uint32_t lw
 #pragma unroll
   for (int b = 0; b < NB; ++b) aes_block<NR>(L, lw, a, s[b]);
 #endif
-}
-
-// Three blocks software-pipelined: block b's round r XORs (and its round r + 1
-// lookups) run while the other two blocks' lookups are in flight, instead of
-// all 48 lookups of a round, a wait for all of them, then all XORs (a wave
-// then has nothing for the LDS while it XORs, and its 4-bit lgkmcnt cannot
-// wait for only the oldest of 48 reads).  Each block's state still finishes a
-// round before its next lookups, in program order: A r, B r, C r, A r + 1, ...
-// The last lookups of each block are its final round's (same table reads).
-template <int NR>
-__device__ __forceinline__ void aes3_pipe(const AesLds<4>& L, const uint32_t lw[2], const AesArgs& a, uint32_t s[3][4]) {
-  uint32_t st[3][4];
-#pragma unroll
-  for (int b = 0; b < 3; ++b)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) st[b][i] = s[b][i] ^ a.rk[i];
-  uint32_t ar[4][4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) ar[c][t] = lw[t >> 1];
-  uint32_t x[3][4][4];
-  auto issue = [&](int b) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      x[b][c][0] = te_sdwa<3, 0>(L, st[b][c], ar[c][0]);
-      x[b][c][1] = te_sdwa<2, 1>(L, st[b][(c + 1) & 3], ar[c][1]);
-      x[b][c][2] = te_sdwa<1, 2>(L, st[b][(c + 2) & 3], ar[c][2]);
-      x[b][c][3] = te_sdwa<0, 3>(L, st[b][(c + 3) & 3], ar[c][3]);
-    }
-  };
-  auto mix = [&](int b, int r) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) st[b][c] = xor3s(xor3(x[b][c][0], x[b][c][1], x[b][c][2]), x[b][c][3], a.rk[4 * r + c]);
-  };
-  issue(0);
-  issue(1);
-  issue(2);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int r = 1; r < NR; ++r) {
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      mix(b, r);
-      issue(b);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#pragma unroll
-  for (int b = 0; b < 3; ++b)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      s[b][c] = xor3s(__builtin_amdgcn_perm(x[b][c][0], x[b][c][1], 0x06010C0Cu),
-                      __builtin_amdgcn_perm(x[b][c][2], x[b][c][3], 0x0C0C0402u), a.rk[4 * NR + c]);
 }
 
 // Counter block iv + b (mod 2^128) as big-endian words.
@@ -737,27 +678,11 @@ __device__ void encrypt_unit_slow(const AesLds<NTAB>& L, const uint32_t lw[2], c
   }
 }
 
-// The plaintext of unit g (blocks 3g - 1 .. 3g + 1) into R.  The tuning
-// diagnostic DN_AES_DIAG_COAL_IN loads the same amount with the wave's
-// lanes contiguous (wrong bytes, timing only: is the strided load a cost?).
+// The plaintext of unit g (blocks 3g - 1 .. 3g + 1) into R.  (Loading the
+// wave's 3 KB lane-contiguous instead was slower: 1.40-1.42 vs 1.37 ms,
+// profiles/r05/l/; the per-lane 48-B loads are issued a unit ahead.)
 __device__ __forceinline__ void load_unit(const AesArgs& a, uint64_t g, uint32_t (&R)[16]) {
-#ifdef DN_AES_DIAG_COAL_IN
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t w0 = 48 * (g - lane);
-  if (g < lane || w0 + 3072 > a.n) {  // the wave's window not wholly inside the message
-    load_raw<3>(a.in, a.skew, 48 * g - 16, R);
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    uint32_t r[8];
-    load_raw<1>(a.in, 0u, w0 + 1024 * k + 16 * lane, r);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) R[4 * k + i] = r[i];
-  }
-#else
   load_raw<3>(a.in, a.skew, 48 * g - 16, R);
-#endif
 }
 
 template <int NR, int NTAB, bool HEX>
@@ -792,9 +717,7 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
       uint32_t ks[3][4];
 #pragma unroll
       for (int j = 0; j < 3; ++j) ctr_block(a.iv, 3 * g - 1 + j, ks[j]);
-      if constexpr (DN_AES_NB == 3 && DN_AES_PIPE && DN_AES_SDWA) {
-        aes3_pipe<NR>(L, lw, a, ks);
-      } else if constexpr (DN_AES_NB == 3) {
+      if constexpr (DN_AES_NB == 3) {
         aes_blocks<NR, 3>(L, lw, a, ks);
       } else {
         aes_blocks<NR, 2>(L, lw, a, ks);
