@@ -35,7 +35,7 @@ def _ref_make_masked_results(members, agg_vars):
     return valid, result
 
 
-@pytest.mark.parametrize("k", [1, 2, 5, 16, 17, 40])
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 8, 9, 10, 16, 17, 40])
 def test_sum_member_results_matches_reference(k):
     rng = np.random.default_rng(k)
     shapes = {"w": {"a": (33, 7), "b": (1,)}, "v": {"c": (1001,)}}
