@@ -58,11 +58,6 @@
 #ifndef DN_AES_HEX_COAL
 #define DN_AES_HEX_COAL 1
 #endif
-// DN_AES_DEC_NB3 (default 1): decrypt interleaves a unit's three keystream
-// blocks too (aes_blocks<NR, 3>), as encrypt does.
-#ifndef DN_AES_DEC_NB3
-#define DN_AES_DEC_NB3 1
-#endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
 #ifndef DN_AES_NB
@@ -896,20 +891,6 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) decrypt_kernel(const A
     if ((acc & (kDecPad | kDecBad)) | bad) atomicOr(a.bad, 1u);
     uint32_t W[12];
     join24(x, W);
-#if DN_AES_DEC_NB3
-    if constexpr (NTAB == 4) {  // the unit's three keystream blocks with their rounds interleaved
-      uint32_t ks[3][4];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) ctr_block(iv, 3 * g - 1 + j, ks[j]);
-      aes_blocks<NR, 3>(L, lw, a, ks);
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        store4(a.out + 16 * (3 * g - 1 + j), __builtin_bswap32(W[4 * j] ^ ks[j][0]),
-               __builtin_bswap32(W[4 * j + 1] ^ ks[j][1]), __builtin_bswap32(W[4 * j + 2] ^ ks[j][2]),
-               __builtin_bswap32(W[4 * j + 3] ^ ks[j][3]));
-      continue;
-    }
-#endif
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const uint64_t kb = 3 * g - 1 + j;

@@ -23,25 +23,13 @@ struct SumArgs {
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// K > 0: the member count as a template argument — all K loads of a pair
-// issued before the first add (the runtime-k loop kept at most 4 in flight);
-// K = 0: any k.
-template <int K>
 __global__ void __launch_bounds__(256) i64_sum_kernel(const SumArgs a) {
   const uint64_t pairs = a.n / 2;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < pairs; i += stride) {
     u64x2 acc = {0, 0};
-    if constexpr (K > 0) {
-      u64x2 v[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.in[j]) + i);
-#pragma unroll
-      for (int j = 0; j < K; ++j) acc += v[j];
-    } else {
 #pragma unroll 4
-      for (int j = 0; j < a.k; ++j) acc += __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.in[j]) + i);
-    }
+    for (int j = 0; j < a.k; ++j) acc += __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.in[j]) + i);
     __builtin_nontemporal_store(acc, reinterpret_cast<u64x2*>(a.out) + i);
   }
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -70,19 +58,10 @@ extern "C" int dn_i64_sum(const int64_t* const* inputs, int k, int64_t* out, uin
   a.n = n;
   a.k = k;
   const uint64_t blocks = (n / 2 + 255) / 256;
-  const dim3 g(blocks < 8192 ? (blocks ? blocks : 1) : 8192), b(256);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (k) {
-    case 2: hipLaunchKernelGGL(i64_sum_kernel<2>, g, b, 0, s, a); break;
-    case 3: hipLaunchKernelGGL(i64_sum_kernel<3>, g, b, 0, s, a); break;
-    case 4: hipLaunchKernelGGL(i64_sum_kernel<4>, g, b, 0, s, a); break;
-    case 5: hipLaunchKernelGGL(i64_sum_kernel<5>, g, b, 0, s, a); break;
-    case 6: hipLaunchKernelGGL(i64_sum_kernel<6>, g, b, 0, s, a); break;
-    case 8: hipLaunchKernelGGL(i64_sum_kernel<8>, g, b, 0, s, a); break;
-    case 9: hipLaunchKernelGGL(i64_sum_kernel<9>, g, b, 0, s, a); break;
-    case 10: hipLaunchKernelGGL(i64_sum_kernel<10>, g, b, 0, s, a); break;
-    default: hipLaunchKernelGGL(i64_sum_kernel<0>, g, b, 0, s, a); break;
-  }
+  // (the member count as a template argument, all loads of a pair issued
+  // before the adds: 0.258 ms either way at 10 x 2^24, profiles/r05/m/)
+  hipLaunchKernelGGL(i64_sum_kernel, dim3(blocks < 8192 ? (blocks ? blocks : 1) : 8192), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), a);
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_i64_sum: %s", hipGetErrorString(err));
   return DN_OK;
