@@ -58,6 +58,11 @@
 #ifndef DN_AES_HEX_COAL
 #define DN_AES_HEX_COAL 1
 #endif
+// DN_AES_DEC_SPLIT (default 1): decrypt in two passes, decode then CTR in
+// place (decode_kernel, ctr_text_kernel); 0 = the one-pass decrypt_kernel.
+#ifndef DN_AES_DEC_SPLIT
+#define DN_AES_DEC_SPLIT 1
+#endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
 #ifndef DN_AES_NB
@@ -842,6 +847,178 @@ __device__ void decrypt_unit_slow(const AesLds<NTAB>& L, const uint32_t lw[2], c
   }
 }
 
+// The nonce (first 24 characters) and the padding (last two) of the text,
+// through a base64 decode table `dec` (LDS): every thread of a kernel reads
+// them (cached lines), the units that hold them validate them again.
+template <bool HEX>
+__device__ __forceinline__ void text_header(const AesArgs& a, const uint8_t* dec, uint32_t iv[4], uint64_t& pad) {
+  uint32_t ignore = 0u, x[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    uint32_t v = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v = (v << 6) | (dec[text_char<HEX>(a, 4 * q + k, ignore)] & 63u);
+    x[q] = v;
+  }
+  iv[0] = (x[0] << 8) | (x[1] >> 16);
+  iv[1] = (x[1] << 16) | (x[2] >> 8);
+  iv[2] = (x[2] << 24) | x[3];
+  iv[3] = (x[4] << 8) | (x[5] >> 16);
+  const uint32_t c1 = text_char<HEX>(a, a.n - 2, ignore), c2 = text_char<HEX>(a, a.n - 1, ignore);
+  pad = c2 == kPadChar ? (c1 == kPadChar ? 2u : 1u) : 0u;
+}
+
+__device__ void build_dec(uint8_t* dec, uint32_t TH) {
+  for (uint32_t e = threadIdx.x; e < 256u; e += TH) {
+    uint32_t d = kDecBad;
+    if (e >= 'A' && e <= 'Z') d = e - 'A';
+    else if (e >= 'a' && e <= 'z') d = e - 'a' + 26u;
+    else if (e >= '0' && e <= '9') d = e - '0' + 52u;
+    else if (e == '+') d = 62u;
+    else if (e == '/') d = 63u;
+    else if (e == '=') d = kDecPad;
+    dec[e] = static_cast<uint8_t>(d);
+  }
+  __syncthreads();
+}
+
+// ---- decrypt in two passes (DN_AES_DEC_SPLIT) --------------------------------------
+// decode_kernel: text -> ciphertext bytes (hex and base64 validated as the
+// one-pass kernel does), a streaming pass with a 256-B table, high occupancy
+// and the next unit's text loaded before this unit's stores; then
+// ctr_text_kernel XORs the keystream in place (the nonce and the length read
+// from the text by every workgroup).  The one-pass decrypt_kernel held 122
+// VGPRs for the AES and loaded each unit's 128 text bytes just before using
+// them (2.62 ms for 1.13 GB, profiles/r05/m/).
+template <bool HEX>
+__device__ void decode_unit_slow(const uint8_t* dec, const AesArgs& a, uint64_t g, uint64_t pad, uint64_t nout) {
+  uint32_t bad = 0u, x[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    uint32_t v = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t pos = 64 * g + 4 * q + k;
+      uint32_t s = 0u;
+      if (pos < a.n) {
+        s = dec[text_char<HEX>(a, pos, bad)];
+        if (pos >= a.n - pad) {
+          bad |= s != kDecPad ? 1u : 0u;
+          s = 0u;
+        } else if (s & (kDecPad | kDecBad)) {
+          bad = 1u;
+          s = 0u;
+        }
+      }
+      v = (v << 6) | s;
+    }
+    x[q] = v;
+  }
+  if (bad) atomicOr(a.bad, 1u);
+  uint32_t W[12];
+  join24(x, W);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int64_t kb = 3 * static_cast<int64_t>(g) - 1 + j;
+    if (kb < 0) continue;
+    const uint64_t b0 = 16ull * static_cast<uint64_t>(kb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t o = b0 + 4 * i + k;
+        if (o < nout) a.out[o] = static_cast<uint8_t>(W[4 * j + i] >> (24 - 8 * k));
+      }
+  }
+}
+
+template <bool HEX>
+__global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
+  __shared__ uint8_t dec[256];
+  build_dec(dec, 256u);
+  uint32_t iv[4];
+  uint64_t pad;
+  text_header<HEX>(a, dec, iv, pad);
+  const uint64_t nout = a.n / 4 * 3 - pad - 16;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u;
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (first == 0) *a.out_len = nout;
+  constexpr int NV = HEX ? 8 : 4;  // 16-B vectors of one unit's text
+  uint32_t R[4 * NV + 4];
+  auto whole = [&](uint64_t g) { return g != 0 && g + 1 < a.units; };
+  const uint64_t tb = HEX ? 128 : 64;  // text bytes per unit
+  if (first < a.units && whole(first)) load_raw<NV>(a.in, a.skew, tb * first, R);
+  for (uint64_t g = first; g < a.units; g += stride) {
+    const uint64_t gn = g + stride;
+    if (!whole(g)) {
+      decode_unit_slow<HEX>(dec, a, g, pad, nout);
+      if (gn < a.units && whole(gn)) load_raw<NV>(a.in, a.skew, tb * gn, R);
+      continue;
+    }
+    uint32_t T[16], bad = 0u;
+    {
+      uint32_t tx[4 * NV];
+      shift_raw<NV>(R, a.skew, tx);
+      if constexpr (HEX) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[k] = pack_nibbles(unhex4(tx[2 * k], bad), unhex4(tx[2 * k + 1], bad));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[k] = tx[k];
+      }
+    }
+    if (gn < a.units && whole(gn)) load_raw<NV>(a.in, a.skew, tb * gn, R);  // next unit's text before the stores
+    uint32_t x[16], acc = 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = unb64_word(dec, T[k], acc);
+    if ((acc & (kDecPad | kDecBad)) | bad) atomicOr(a.bad, 1u);
+    uint32_t W[12];
+    join24(x, W);
+    uint8_t* o = a.out + 48 * g - 16;  // raw bytes 48 g .. 48 g + 47 = ciphertext from 48 g - 16
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      store4(o + 16 * j, __builtin_bswap32(W[4 * j]), __builtin_bswap32(W[4 * j + 1]), __builtin_bswap32(W[4 * j + 2]),
+             __builtin_bswap32(W[4 * j + 3]));
+  }
+}
+
+// out[0 .. nout) ^= keystream(nonce), in place; nonce and nout from the text
+template <int NR, int NTAB, bool HEX>
+__global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) ctr_text_kernel(const AesArgs a) {
+  __shared__ AesLds<NTAB> L;
+  build_tables<NTAB>(L);
+  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  const uint32_t lw[2] = {lb, lb | 0x10000u};
+  constexpr uint32_t TH = NTAB == 4 ? 1024u : 512u;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * TH;
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * TH + threadIdx.x;
+  uint32_t iv[4];
+  uint64_t pad;
+  text_header<HEX>(a, L.dec, iv, pad);
+  const uint64_t nout = a.n / 4 * 3 - pad - 16;
+  const uint64_t blocks = (nout + 15) / 16;
+  uint32_t R[8];
+  if (first < blocks && 16 * (first + 1) <= nout) load_raw<1>(a.out, 0u, 16 * first, R);
+  for (uint64_t b = first; b < blocks; b += stride) {
+    uint32_t ks[4];
+    ctr_block(iv, b, ks);
+    aes_block<NR>(L, lw, a, ks);
+    if (16 * (b + 1) <= nout) {
+      const uint32_t p0 = R[0], p1 = R[1], p2 = R[2], p3 = R[3];
+      const uint64_t bn = b + stride;
+      if (bn < blocks && 16 * (bn + 1) <= nout) load_raw<1>(a.out, 0u, 16 * bn, R);
+      store4(a.out + 16 * b, p0 ^ __builtin_bswap32(ks[0]), p1 ^ __builtin_bswap32(ks[1]),
+             p2 ^ __builtin_bswap32(ks[2]), p3 ^ __builtin_bswap32(ks[3]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint64_t o = 16 * b + k;
+        if (o < nout) a.out[o] = static_cast<uint8_t>(a.out[o] ^ (ks[k >> 2] >> (24 - 8 * (k & 3))));
+      }
+    }
+  }
+}
+
 template <int NR, int NTAB, bool HEX>
 __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) decrypt_kernel(const AesArgs a) {
   DN_AES_PROLOGUE;
@@ -953,6 +1130,17 @@ static void launch(int kind, bool hex, uint64_t units, hipStream_t s, const AesA
   } else if (kind == kEncrypt) {
     if (hex) hipLaunchKernelGGL((encrypt_kernel<NR, NTAB, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((encrypt_kernel<NR, NTAB, false>), g, b, 0, s, a);
+  } else if (DN_AES_DEC_SPLIT) {
+    // pass 1: decode, 256-thread workgroups; pass 2: CTR in place over the
+    // ciphertext's 16-B blocks (at most units * 3 of them)
+    const uint64_t dw = (units + 255) / 256, dcap = static_cast<uint64_t>(device_cu_count()) * 8u;
+    const dim3 dg(static_cast<uint32_t>(dw < dcap ? (dw ? dw : 1) : dcap));
+    if (hex) hipLaunchKernelGGL((decode_kernel<true>), dg, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((decode_kernel<false>), dg, dim3(256), 0, s, a);
+    const uint64_t cw = (3 * units + TH - 1) / TH;
+    const dim3 cg(static_cast<uint32_t>(cw < cap ? (cw ? cw : 1) : cap));
+    if (hex) hipLaunchKernelGGL((ctr_text_kernel<NR, NTAB, true>), cg, b, 0, s, a);
+    else hipLaunchKernelGGL((ctr_text_kernel<NR, NTAB, false>), cg, b, 0, s, a);
   } else {
     if (hex) hipLaunchKernelGGL((decrypt_kernel<NR, NTAB, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((decrypt_kernel<NR, NTAB, false>), g, b, 0, s, a);
