@@ -63,6 +63,11 @@
 #ifndef DN_AES_DEC_SPLIT
 #define DN_AES_DEC_SPLIT 1
 #endif
+// DN_AES_DEC_COAL (default 1): decode_kernel reads a wave's hex text line by
+// line and transposes it (as the encrypt kernel's text stores).
+#ifndef DN_AES_DEC_COAL
+#define DN_AES_DEC_COAL 1
+#endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
 #ifndef DN_AES_NB
@@ -947,12 +952,45 @@ __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
   uint32_t R[4 * NV + 4];
   auto whole = [&](uint64_t g) { return g != 0 && g + 1 < a.units; };
   const uint64_t tb = HEX ? 128 : 64;  // text bytes per unit
-  if (first < a.units && whole(first)) load_raw<NV>(a.in, a.skew, tb * first, R);
+  const uint32_t lane = threadIdx.x & 63u;
+  // unit gq's text into R; a wave whose 64 lanes all load whole units reads
+  // its 8 KB line by line and transposes (hex_coalesce: load v of lane l is
+  // chunk l >> 3 of lane 8 v + (l & 7)), the chunk after a unit (skew) from
+  // the next lane (the next wave's first chunk for lane 63)
+  auto load_unit_text = [&](uint64_t gq) {
+    if constexpr (HEX && DN_AES_DEC_COAL) {
+      if (__ballot(1) == ~0ull) {
+        const uint64_t w0 = tb * (gq - lane);
+        const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 7u) + 16 * (lane >> 3));
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
+          R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
+        }
+        hex_coalesce(R, lane);
+        if (a.skew != 0u) {
+          uint32_t e[4];
+          if (lane == 63u) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 8192));
+            e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
+            R[32 + i] = lane == 63u ? e[i] : nx;
+          }
+        }
+        return;
+      }
+    }
+    load_raw<NV>(a.in, a.skew, tb * gq, R);
+  };
+  if (first < a.units && whole(first)) load_unit_text(first);
   for (uint64_t g = first; g < a.units; g += stride) {
     const uint64_t gn = g + stride;
     if (!whole(g)) {
       decode_unit_slow<HEX>(dec, a, g, pad, nout);
-      if (gn < a.units && whole(gn)) load_raw<NV>(a.in, a.skew, tb * gn, R);
+      if (gn < a.units && whole(gn)) load_unit_text(gn);
       continue;
     }
     uint32_t T[16], bad = 0u;
@@ -967,7 +1005,7 @@ __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
         for (int k = 0; k < 16; ++k) T[k] = tx[k];
       }
     }
-    if (gn < a.units && whole(gn)) load_raw<NV>(a.in, a.skew, tb * gn, R);  // next unit's text before the stores
+    if (gn < a.units && whole(gn)) load_unit_text(gn);  // next unit's text before the stores
     uint32_t x[16], acc = 0u;
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = unb64_word(dec, T[k], acc);
