@@ -516,6 +516,28 @@ __device__ __forceinline__ void hex_coalesce(uint32_t h[32], uint32_t lane) {
     }
 }
 
+// The same for 4 chunks per lane (64 base64 characters): chunk register v of
+// lane l is chunk l >> 4 of lane 16 v + (l & 15) — lane bit 4 <-> chunk bit
+// 0 (v_permlane16_swap), 5 <-> 1 (v_permlane32_swap); also its own inverse.
+__device__ __forceinline__ void b64_coalesce(uint32_t h[16]) {
+#pragma unroll
+  for (int c : {0, 2})
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const auto r = __builtin_amdgcn_permlane16_swap(h[4 * c + w], h[4 * (c + 1) + w], false, false);
+      h[4 * c + w] = r[0];
+      h[4 * (c + 1) + w] = r[1];
+    }
+#pragma unroll
+  for (int c : {0, 1})
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const auto r = __builtin_amdgcn_permlane32_swap(h[4 * c + w], h[4 * (c + 2) + w], false, false);
+      h[4 * c + w] = r[0];
+      h[4 * (c + 2) + w] = r[1];
+    }
+}
+
 // 12 big-endian words (48 bytes) -> 32 hex words (64 base64 characters): sextet
 // j of a word triple (w0, w1, w2) is moved to bits 8..13 by one shift or
 // funnel shift (sextet 3 sits there already), looked up, and two lookups are
@@ -788,6 +810,17 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
 #endif
       }
     } else {
+#if DN_AES_HEX_COAL
+      if (__ballot(1) == ~0ull) {  // all 64 lanes, whole units: one contiguous KB per store
+        const uint32_t lane = threadIdx.x & 63u;
+        b64_coalesce(C);
+        uint8_t* o = a.out + 64 * (g - lane) + 64 * (lane & 15u) + 16 * (lane >> 4);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          store4(o + 1024 * v, C[4 * v], C[4 * v + 1], C[4 * v + 2], C[4 * v + 3], a.plain != 0u);
+        continue;
+      }
+#endif
       uint8_t* o = a.out + 64 * g;
 #pragma unroll
       for (int v = 0; v < 4; ++v)
@@ -958,6 +991,31 @@ __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
   // chunk l >> 3 of lane 8 v + (l & 7)), the chunk after a unit (skew) from
   // the next lane (the next wave's first chunk for lane 63)
   auto load_unit_text = [&](uint64_t gq) {
+    if constexpr (!HEX && DN_AES_DEC_COAL) {
+      if (__ballot(1) == ~0ull) {  // base64 text: 4 chunks per lane, as the encrypt stores
+        const uint64_t w0 = tb * (gq - lane);
+        const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 64 * (lane & 15u) + 16 * (lane >> 4));
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
+          R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
+        }
+        b64_coalesce(R);
+        if (a.skew != 0u) {
+          uint32_t e[4];
+          if (lane == 63u) {
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 4096));
+            e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
+            R[16 + i] = lane == 63u ? e[i] : nx;
+          }
+        }
+        return;
+      }
+    }
     if constexpr (HEX && DN_AES_DEC_COAL) {
       if (__ballot(1) == ~0ull) {
         const uint64_t w0 = tb * (gq - lane);
