@@ -398,7 +398,30 @@ def envelope_row(recs, reps: int, s, e) -> dict:
         kern.append(s.elapsed_time(e) / reps)
     enc_kernel_ms = min(kern)
     kernel_equal = bool(torch.equal(kbuf[16:], env[2:]))
-    del kbuf
+    # the decrypt kernels alone (decode + in-place CTR, csrc/aes_envelope.hip) on the
+    # "0x"-prefixed text as the JSON carries it, into a preallocated output
+    tl = env.numel() - 2
+    cap = int(AL.dn_aes_decrypt_capacity(tl, 1))
+    dbuf = torch.empty(cap + 16, dtype=torch.uint8, device=recs.device)
+    olen = torch.zeros(1, dtype=torch.int64, device=recs.device)
+    dbad = torch.zeros(1, dtype=torch.int32, device=recs.device)
+
+    def k_dec():
+        _cn.check(AL.dn_aes_decrypt(key, len(key), env.data_ptr() + 2, tl, 1, dbuf.data_ptr(), cap + 16,
+                                    olen.data_ptr(), dbad.data_ptr(), stream.cuda_stream))
+
+    dkern = []
+    warm(k_dec)
+    for _ in range(3):
+        s.record(stream)
+        for _ in range(reps):
+            k_dec()
+        e.record(stream)
+        torch.cuda.synchronize()
+        dkern.append(s.elapsed_time(e) / reps)
+    dec_kernel_ms = min(dkern)
+    dec_kernel_equal = bool(torch.equal(dbuf[:n], recs)) and int(olen.item()) == n and int(dbad.item()) == 0
+    del kbuf, dbuf
     units = 4096  # the first 4096 thread units (196 KB) against the oracle
     m = base64.b64decode(bytes.fromhex(bytes(env[2:2 + 128 * units].cpu().numpy()).decode()))
     oracle_ok = m[:16] == nonce and m[16:] == c_oracle.aes_ctr(key, nonce, bytes(recs[:len(m) - 16].cpu().numpy()))
@@ -408,6 +431,7 @@ def envelope_row(recs, reps: int, s, e) -> dict:
                        f"({text_bytes / 1e9:.2f} GB)",
            "encrypt_ms": enc_ms, "decrypt_ms": dec_ms,
            "encrypt_kernel_ms": enc_kernel_ms, "encrypt_kernel_equal_api": kernel_equal,
+           "decrypt_kernel_ms": dec_kernel_ms, "decrypt_kernel_roundtrip": dec_kernel_equal,
            "timing": "encrypt_ms / decrypt_ms: the Python API calls (output allocation, decrypt's length "
                      "read-back), mean of one round; encrypt_kernel_ms: dn_aes_encrypt on a preallocated "
                      "buffer, >= 0.15 s warm-up, best of 3 rounds; the rooflines use the kernel time",
@@ -416,6 +440,8 @@ def envelope_row(recs, reps: int, s, e) -> dict:
                                 "14 rounds x 16 Te lookups x 4 B per 16-byte block (encrypt kernel)"),
            "roofline_hbm": roof("hbm", (n + text_bytes) / (enc_kernel_ms * 1e-3) / 1e9,
                                 "record bytes in + 2.67 x text bytes out (encrypt kernel)"),
+           "roofline_lds_decrypt": roof("lds", lds_bytes / (dec_kernel_ms * 1e-3) / 1e9,
+                                        "14 rounds x 16 Te lookups x 4 B per 16-byte block (decode + CTR kernels)"),
            "bound": "lds + valu (T-table AES-256; base64 and hex fused)",
            "roundtrip_equal": bool(torch.equal(back, recs)), "oracle_prefix_equal": bool(oracle_ok)}
     del env, back
