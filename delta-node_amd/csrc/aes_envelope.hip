@@ -203,10 +203,20 @@ __device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
   return __builtin_amdgcn_bitop3_b32(a, b, k, 0x96);
 }
 
+// DN_AES_B1 (default 1): a byte-1 lookup's address is (s & 0xFF00) | ar, one
+// full-rate v_bitop3 (ar keeps its lane and table bits, byte 1 zero), instead
+// of the half-rate SDWA move the other three byte positions need.
+#ifndef DN_AES_B1
+#define DN_AES_B1 1
+#endif
+
 template <int K, int T>
 __device__ __forceinline__ uint32_t te_sdwa(const AesLds<4>& L, uint32_t s, uint32_t& ar) {
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(&L.tab[0][0][0]) + 128 * (T & 1);
+  if constexpr (K == 1 && DN_AES_B1)
+    return *reinterpret_cast<const uint32_t*>(base + __builtin_amdgcn_bitop3_b32(s, 0xFF00u, ar, 0xEA));
   addr_byte<K>(ar, s);
-  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&L.tab[0][0][0]) + ar + 128 * (T & 1));
+  return *reinterpret_cast<const uint32_t*>(base + ar);
 }
 
 // Final round (SubBytes + ShiftRows + AddRoundKey) through the same address
