@@ -1088,7 +1088,7 @@ def main():
     # the timed average is over several placements, not one allocation's.
     nbuf = max(1, args.placements)
     # each the block make_shares_vec returns for out=None (memory.share_block:
-    # pooled 2 MiB physical chunks; torch.empty below 64 MiB)
+    # pooled 16 MiB physical chunks; torch.empty below 64 MiB)
     share_bufs = [memory.share_block((n, vb), dev) for _ in range(nbuf)]
     rec = torch.empty(N, dtype=torch.int64, device=dev)
     w = _native.lagrange(xs, t)
@@ -1249,7 +1249,7 @@ def main():
                                f"vector, GF(2^521-1), sharded by element over {world} GPU(s)",
                    "elements_total": N_total, "elements_per_gpu": N, "threshold": t, "shares": n, "xs": xs,
                    "parallelism": f"element-shard x{world}",
-                   "share_blocks": "memory.share_block (make_shares_vec's own output allocation: pooled 2 MiB "
+                   "share_blocks": "memory.share_block (make_shares_vec's own output allocation: pooled 16 MiB "
                                    "physical chunks)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS,

@@ -1,10 +1,10 @@
-"""Share-block memory built from 2 MiB physical chunks (dn_block_alloc).
+"""Share-block memory built from 16 MiB physical chunks (dn_block_alloc).
 
 The split writes 330 B per element at 3-of-5 (70 % of its traffic) and its
 rate follows the physical pages of the share block: a 5.5 GB
 block from one hipMalloc lands in a fast or a slow class (0.66 / 0.78 of
-8 TB/s for the split).  A block built from 2 MiB physical chunks mapped back to
-back (hipMemCreate / hipMemMap) ran in the fast class every time it was
+8 TB/s for the split).  A block built from physical chunks (CHUNK_BYTES)
+mapped back to back (hipMemCreate / hipMemMap) ran in the fast class every time it was
 measured — 10 of 10 blocks at 0.786-0.800 against 6 of 10 torch.empty blocks
 (profiles/r04/a/block_probe.jsonl, and round 1's place_vmm2/3) — so the vector
 API allocates the share blocks it returns here (`share_block`), and callers
@@ -378,7 +378,7 @@ def record_stream(t, stream) -> None:
 
 def share_block(shape: Union[int, Sequence[int]], device=None):
     """A share block (uint8 [n_shares, vec_bytes(n)] or any shape): pooled
-    2 MiB-chunk memory from CHUNKED_MIN_BYTES up, torch.empty below."""
+    chunked memory (CHUNK_BYTES) from CHUNKED_MIN_BYTES up, torch.empty below."""
     import torch
 
     dev = _device_index(device)

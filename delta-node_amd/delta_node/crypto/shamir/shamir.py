@@ -285,7 +285,7 @@ class SecretShare(object):
         coeffs  optional uint8 device tensor [t-1, vec_bytes(N)]; default: drawn
                 from `self.random` as N sequential `make_shares` calls would
         out     optional uint8 device tensor [shares, vec_bytes(N)]; default: a
-                pooled block of 2 MiB physical chunks (memory.share_block)
+                pooled block of 16 MiB physical chunks (memory.share_block)
         Returns uint8 device tensor [shares, vec_bytes(N)]: row x-1 holds share x
         of every element (tiled M521 layout, canonical residues).
         """
@@ -301,7 +301,7 @@ class SecretShare(object):
         n = vals.numel()
         t = max(self.threshold, 1)
         vb = field.vec_bytes(n)
-        if out is None:  # pooled 2 MiB-chunk block (memory.py: the split's fast placement)
+        if out is None:  # pooled chunked block (memory.py: the split's fast placement)
             out = memory.share_block((max(shares, 0), vb), dev)
         elif (out.dtype != torch.uint8 or tuple(out.shape) != (shares, vb) or not out.is_contiguous()
               or out.device != dev):

@@ -1,5 +1,5 @@
 """Share-block memory (delta_node.crypto.shamir.memory, csrc/vmm_block.cpp):
-blocks of 2 MiB physical chunks, pooled, aliased by torch tensors through
+blocks of 16 MiB physical chunks, pooled, aliased by torch tensors through
 __cuda_array_interface__; the vector API's default output allocation.  The
 split written into a chunked block equals the split into torch.empty memory
 byte for byte (the reference's shamir.py:55-66 per element)."""
