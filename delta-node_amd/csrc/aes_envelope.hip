@@ -55,8 +55,11 @@
 // hold whole units stores its 8 KB of hex text line by line (hex_coalesce:
 // cross-lane transpose, each store instruction one contiguous KB) instead of
 // each lane its own 128 bytes (16 B in each of 64 lines per instruction).
+// 2 (default): two transpose stages instead of three (hex_coalesce_half: no
+// selects), each store writing the 64-B halves of 16 lines: 1.339-1.342 vs
+// 1.364-1.382 ms (profiles/r05/r/).
 #ifndef DN_AES_HEX_COAL
-#define DN_AES_HEX_COAL 1
+#define DN_AES_HEX_COAL 2
 #endif
 // DN_AES_DEC_SPLIT (default 1): decrypt in two passes, decode then CTR in
 // place (decode_kernel, ctr_text_kernel); 0 = the one-pass decrypt_kernel.
@@ -64,7 +67,9 @@
 #define DN_AES_DEC_SPLIT 1
 #endif
 // DN_AES_DEC_COAL (default 1): decode_kernel reads a wave's hex text line by
-// line and transposes it (as the encrypt kernel's text stores).
+// line and transposes it (as the encrypt kernel's text stores); 2 reads half
+// lines (hex_coalesce_half): slower, 1.98-2.01 vs 1.94-1.96 ms
+// (profiles/r05/s/).
 #ifndef DN_AES_DEC_COAL
 #define DN_AES_DEC_COAL 1
 #endif
@@ -482,11 +487,34 @@ __device__ void build_hex(HexLds& H, uint32_t TH) {
 }
 
 // the table word of a sextet held at bits 8..13 of v (higher and lower bits
-// ignored): address (v & 0x3F00) | lane bits by one v_bitop3
+// ignored): LDS address (v & 0x3F00) | lbx by one v_bitop3, where lbx = the
+// lane bits | the table's own LDS address (DN_AES_HEX_BASE: the table is
+// 16 KB-aligned, so its address has no bit in 8..13 and ORs in — no add per
+// lookup; table t at the read's immediate offset)
+#ifndef DN_AES_HEX_BASE
+#define DN_AES_HEX_BASE 1
+#endif
+typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
+
 template <int T>
 __device__ __forceinline__ uint32_t hex_lookup(const HexLds& H, uint32_t v, uint32_t lb) {
   const uint32_t a = __builtin_amdgcn_bitop3_b32(v, 0x3F00u, lb, 0xea);  // (v & m) | lb
+#if DN_AES_HEX_BASE
+  (void)H;
+  return *(reinterpret_cast<lds_u32_t*>(static_cast<uintptr_t>(a)) + 32 * T);
+#else
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(&H.row[0][0]) + a + 128 * T);
+#endif
+}
+
+// lb | the LDS address of H (DN_AES_HEX_BASE), else lb
+__device__ __forceinline__ uint32_t hex_lane_bits(const HexLds& H, uint32_t lb) {
+#if DN_AES_HEX_BASE
+  return lb | static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&H.row[0][0]));
+#else
+  (void)H;
+  return lb;
+#endif
 }
 
 // The wave's 64 x 8 16-byte chunks (lane s holds the 128 text bytes of unit
@@ -523,6 +551,29 @@ __device__ __forceinline__ void hex_coalesce(uint32_t h[32], uint32_t lane) {
       const uint32_t y = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x128, 0xF, 0xF, false));
       h[4 * c + w] = b3 ? y : A;
       h[4 * (c + 1) + w] = b3 ? B : y;
+    }
+}
+
+// Two stages only (DN_AES_HEX_COAL == 2): lane bit 5 <-> chunk bit 1
+// (v_permlane32_swap), 4 <-> 0 (v_permlane16_swap), no selects: chunk register
+// v of lane l is chunk 4 (v >> 2) + (l >> 4) of lane (l & 15) + 16 (v & 3),
+// so store v writes the 64-B halves (v >> 2) of 16 consecutive lines.
+__device__ __forceinline__ void hex_coalesce_half(uint32_t h[32]) {
+#pragma unroll
+  for (int c : {0, 1, 4, 5})
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const auto r = __builtin_amdgcn_permlane32_swap(h[4 * c + w], h[4 * (c + 2) + w], false, false);
+      h[4 * c + w] = r[0];
+      h[4 * (c + 2) + w] = r[1];
+    }
+#pragma unroll
+  for (int c : {0, 2, 4, 6})
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const auto r = __builtin_amdgcn_permlane16_swap(h[4 * c + w], h[4 * (c + 1) + w], false, false);
+      h[4 * c + w] = r[0];
+      h[4 * (c + 1) + w] = r[1];
     }
 }
 
@@ -732,7 +783,7 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
   DN_AES_PROLOGUE;
 #if DN_AES_HEX_LDS
   constexpr bool kHexLds = HEX && NTAB == 4;
-  __shared__ HexLds HX;
+  __shared__ __attribute__((aligned(16384))) HexLds HX;  // 16 KB-aligned: hex_lookup
   if constexpr (kHexLds) {
     build_hex(HX, TH);
     __syncthreads();
@@ -782,15 +833,24 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) encrypt_kernel(const A
 #if DN_AES_HEX_LDS
     if constexpr (kHexLds) {
       uint32_t h[32];
-      hex_lds_unit(HX, W, lb, h);
+      hex_lds_unit(HX, W, hex_lane_bits(HX, lb), h);
 #if DN_AES_HEX_COAL
       if (__ballot(1) == ~0ull) {  // all 64 lanes here, each with a whole unit (units g0 .. g0 + 63)
         const uint32_t lane = threadIdx.x & 63u;
+#if DN_AES_HEX_COAL == 2
+        hex_coalesce_half(h);
+        uint8_t* o = a.out + 128 * (g - lane) + 128 * (lane & 15u) + 16 * (lane >> 4);
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+          store4(o + 2048 * (v & 1) + 4096 * ((v >> 1) & 1) + 64 * (v >> 2), h[4 * v], h[4 * v + 1], h[4 * v + 2],
+                 h[4 * v + 3], a.plain != 0u);
+#else
         hex_coalesce(h, lane);
         uint8_t* o = a.out + 128 * (g - lane) + 128 * (lane & 7u) + 16 * (lane >> 3);
 #pragma unroll
         for (int v = 0; v < 8; ++v)
           store4(o + 1024 * v, h[4 * v], h[4 * v + 1], h[4 * v + 2], h[4 * v + 3], a.plain != 0u);
+#endif
         continue;
       }
 #endif
@@ -1029,6 +1089,16 @@ __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
     if constexpr (HEX && DN_AES_DEC_COAL) {
       if (__ballot(1) == ~0ull) {
         const uint64_t w0 = tb * (gq - lane);
+#if DN_AES_DEC_COAL == 2
+        // half lines (hex_coalesce_half, the encrypt's default transpose, also its own inverse)
+        const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 15u) + 16 * (lane >> 4));
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          const u32x4 x = __builtin_nontemporal_load(p + 128 * (v & 1) + 256 * ((v >> 1) & 1) + 4 * (v >> 2));
+          R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
+        }
+        hex_coalesce_half(R);
+#else
         const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 7u) + 16 * (lane >> 3));
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
@@ -1036,6 +1106,7 @@ __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
           R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
         }
         hex_coalesce(R, lane);
+#endif
         if (a.skew != 0u) {
           uint32_t e[4];
           if (lane == 63u) {
