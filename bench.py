@@ -57,6 +57,69 @@ def roof(bound: str, achieved: float, note: str) -> dict:
 FE_BYTES = 66           # ceil(521 / 8): one field element in the tiled layout
 
 
+class TimingEvent:
+    """A HIP timing event created with hipEventDisableSystemFence, with the
+    record / elapsed_time surface of torch.cuda.Event.  torch's events are
+    hipEventDefault: recording one performs a system-scope fence — an L2
+    write-back and invalidate between the kernels it sits between — which is a
+    cost of the measurement, not of the path (hip_runtime_api.h: the flag
+    "can improve the accuracy of timing measurements by avoiding the cost of
+    cache writeback and invalidation").  Same stream, so the order of the
+    kernels and the events is unchanged.  The HIP runtime is the one torch
+    loaded (the SONAME resolves to the library already in the process)."""
+    _hip = None
+    FLAGS = 0x20000000  # hipEventDisableSystemFence
+
+    @classmethod
+    def hip(cls):
+        if cls._hip is None:
+            import ctypes
+
+            maps = {ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln}
+            if len(maps) != 1:
+                raise RuntimeError(f"expected one HIP runtime in the process, found {sorted(maps)}")
+            h = ctypes.CDLL(maps.pop())
+            h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            h.hipEventSynchronize.argtypes = [ctypes.c_void_p]
+            h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            cls._hip = h
+        return cls._hip
+
+    def __init__(self):
+        import ctypes
+
+        self.ev = ctypes.c_void_p()
+        if self.hip().hipEventCreateWithFlags(ctypes.byref(self.ev), self.FLAGS) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+
+    def record(self, stream):
+        if self.hip().hipEventRecord(self.ev, ctypes_stream(stream)) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_time(self, end) -> float:
+        import ctypes
+
+        h = self.hip()
+        if h.hipEventSynchronize(end.ev) != 0:
+            raise RuntimeError("hipEventSynchronize failed")
+        ms = ctypes.c_float()
+        if h.hipEventElapsedTime(ctypes.byref(ms), self.ev, end.ev) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return float(ms.value)
+
+    def __del__(self):
+        if self._hip is not None and self.ev:
+            self._hip.hipEventDestroy(self.ev)
+
+
+def ctypes_stream(stream):
+    import ctypes
+
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
 def warm(fn, seconds: float = 0.15) -> None:
     """Run fn back to back for `seconds` of wall time (at least 3 calls): the
     GPU clock ramps up over tens of milliseconds of sustained work after an
@@ -1019,6 +1082,9 @@ def main():
     ap.add_argument("--config4-log2n", type=int, default=26, help="config 4 total elements = 2^this")
     ap.add_argument("--config5", type=int, default=1, help="also run BASELINE config 5 (end-to-end round over "
                                                             "loopback HTTP to a second process; N=1 only)")
+    ap.add_argument("--events", choices=("nofence", "torch"), default="nofence",
+                    help="timing events of the timed steps: HIP events without the system-scope fence "
+                         "(TimingEvent, default) or torch.cuda.Event (a fence, i.e. an L2 write-back, per record)")
     ap.add_argument("--cold", type=int, default=1, help="also time the first make_shares_vec / config-5 round "
                                                          "of fresh processes (with --rows; N=1 only)")
     args = ap.parse_args()
@@ -1101,8 +1167,9 @@ def main():
     # HIP events on the launch stream bracket every kernel of the timed steps:
     # two per step (before the split, between split and reconstruct); the
     # reconstruct of step i ends at step i + 1's first event (the last one at
-    # one more).  Each event record is a queue packet of its own (~4-5 us of
-    # stream time at 2^21, r05g), so no third per step.
+    # one more).  Each event record is a queue packet of its own, so no third
+    # per step; they are TimingEvents (no system-scope fence per record:
+    # torch's events cost ~4-5 us of stream time each at 2^21, r05g).
     def step(i, ev=None):
         b = i % nbuf
         if ev:
@@ -1116,8 +1183,9 @@ def main():
         for i in range(args.warmup):
             fn(i)
         barrier()
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
-        end = torch.cuda.Event(enable_timing=True)
+        mk = TimingEvent if args.events == "nofence" else (lambda: torch.cuda.Event(enable_timing=True))
+        evs = [[mk() for _ in range(2)] for _ in range(steps)]
+        end = mk()
         barrier()
         t0 = time.perf_counter()
         for i in range(steps):
@@ -1262,6 +1330,8 @@ def main():
                      "kernel": "dn::split_kernel<3, false, false, false, 2>",
                      "algorithmic_bytes_per_launch": split_bytes, "avg_launch_ms": split_ms,
                      "avg_over": f"{args.steps} timed launches rotating over {nbuf} share buffers",
+                     "events": ("HIP events with hipEventDisableSystemFence on the launch stream"
+                                if args.events == "nofence" else "torch.cuda.Event (system-scope fence per record)"),
                      "placement": placement,
                      "ceiling_measured": ceiling and {
                          **ceiling, "GBps": split_bytes / (ceiling["ms"] * 1e-3) / 1e9,
