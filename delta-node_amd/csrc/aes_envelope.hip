@@ -61,10 +61,19 @@
 #ifndef DN_AES_HEX_COAL
 #define DN_AES_HEX_COAL 2
 #endif
-// DN_AES_DEC_SPLIT (default 1): decrypt in two passes, decode then CTR in
-// place (decode_kernel, ctr_text_kernel); 0 = the one-pass decrypt_kernel.
+// DN_AES_DEC_SPLIT: 2 (default) = one pass with decode_kernel's coalesced,
+// transposed text reads (decrypt_fused_kernel): 1.67-1.70 vs 1.95-1.96 ms for
+// the two passes (profiles/r05/x/); 1 = two passes, decode then CTR in place
+// (decode_kernel, ctr_text_kernel); 0 = the one-pass decrypt_kernel with
+// per-lane text reads.
 #ifndef DN_AES_DEC_SPLIT
-#define DN_AES_DEC_SPLIT 1
+#define DN_AES_DEC_SPLIT 2
+#endif
+// DN_AES_DEC_NB: keystream blocks of a decrypt_fused_kernel unit whose rounds
+// run interleaved (3) or one block at a time (1, default: fewer registers with
+// the next unit's text held; 1.67-1.70 vs 1.76-1.81 ms)
+#ifndef DN_AES_DEC_NB
+#define DN_AES_DEC_NB 1
 #endif
 // DN_AES_DEC_COAL (default 1): decode_kernel reads a wave's hex text line by
 // line and transposes it (as the encrypt kernel's text stores); 2 reads half
@@ -1040,6 +1049,80 @@ __device__ void decode_unit_slow(const uint8_t* dec, const AesArgs& a, uint64_t 
   }
 }
 
+// Unit gq's text into R (decode_kernel, decrypt_fused_kernel): a wave whose
+// 64 lanes all load whole units reads its text line by line and transposes
+// (hex_coalesce: load v of lane l is chunk l >> 3 of lane 8 v + (l & 7); base64:
+// b64_coalesce), the chunk after a unit (skew) from the next lane (the next
+// wave's first chunk for lane 63); otherwise each lane its own unit.
+template <bool HEX>
+__device__ __forceinline__ void load_unit_text(const AesArgs& a, uint64_t gq, uint32_t lane,
+                                             uint32_t (&R)[HEX ? 36 : 20]) {
+  constexpr int NV = HEX ? 8 : 4;      // 16-B vectors of one unit's text
+  const uint64_t tb = HEX ? 128 : 64;  // text bytes per unit
+  if constexpr (!HEX && DN_AES_DEC_COAL) {
+    if (__ballot(1) == ~0ull) {  // base64 text: 4 chunks per lane, as the encrypt stores
+      const uint64_t w0 = tb * (gq - lane);
+      const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 64 * (lane & 15u) + 16 * (lane >> 4));
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
+        R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
+      }
+      b64_coalesce(R);
+      if (a.skew != 0u) {
+        uint32_t e[4];
+        if (lane == 63u) {
+          const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 4096));
+          e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
+          R[16 + i] = lane == 63u ? e[i] : nx;
+        }
+      }
+      return;
+    }
+  }
+  if constexpr (HEX && DN_AES_DEC_COAL) {
+    if (__ballot(1) == ~0ull) {
+      const uint64_t w0 = tb * (gq - lane);
+#if DN_AES_DEC_COAL == 2
+      // half lines (hex_coalesce_half, the encrypt's default transpose, also its own inverse)
+      const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 15u) + 16 * (lane >> 4));
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const u32x4 x = __builtin_nontemporal_load(p + 128 * (v & 1) + 256 * ((v >> 1) & 1) + 4 * (v >> 2));
+        R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
+      }
+      hex_coalesce_half(R);
+#else
+      const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 7u) + 16 * (lane >> 3));
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
+        R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
+      }
+      hex_coalesce(R, lane);
+#endif
+      if (a.skew != 0u) {
+        uint32_t e[4];
+        if (lane == 63u) {
+          const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 8192));
+          e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
+          R[32 + i] = lane == 63u ? e[i] : nx;
+        }
+      }
+      return;
+    }
+  }
+  load_raw<NV>(a.in, a.skew, tb * gq, R);
+}
+
 template <bool HEX>
 __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
   __shared__ uint8_t dec[256];
@@ -1054,82 +1137,14 @@ __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
   constexpr int NV = HEX ? 8 : 4;  // 16-B vectors of one unit's text
   uint32_t R[4 * NV + 4];
   auto whole = [&](uint64_t g) { return g != 0 && g + 1 < a.units; };
-  const uint64_t tb = HEX ? 128 : 64;  // text bytes per unit
   const uint32_t lane = threadIdx.x & 63u;
-  // unit gq's text into R; a wave whose 64 lanes all load whole units reads
-  // its 8 KB line by line and transposes (hex_coalesce: load v of lane l is
-  // chunk l >> 3 of lane 8 v + (l & 7)), the chunk after a unit (skew) from
-  // the next lane (the next wave's first chunk for lane 63)
-  auto load_unit_text = [&](uint64_t gq) {
-    if constexpr (!HEX && DN_AES_DEC_COAL) {
-      if (__ballot(1) == ~0ull) {  // base64 text: 4 chunks per lane, as the encrypt stores
-        const uint64_t w0 = tb * (gq - lane);
-        const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 64 * (lane & 15u) + 16 * (lane >> 4));
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
-          R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
-        }
-        b64_coalesce(R);
-        if (a.skew != 0u) {
-          uint32_t e[4];
-          if (lane == 63u) {
-            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 4096));
-            e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
-            R[16 + i] = lane == 63u ? e[i] : nx;
-          }
-        }
-        return;
-      }
-    }
-    if constexpr (HEX && DN_AES_DEC_COAL) {
-      if (__ballot(1) == ~0ull) {
-        const uint64_t w0 = tb * (gq - lane);
-#if DN_AES_DEC_COAL == 2
-        // half lines (hex_coalesce_half, the encrypt's default transpose, also its own inverse)
-        const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 15u) + 16 * (lane >> 4));
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-          const u32x4 x = __builtin_nontemporal_load(p + 128 * (v & 1) + 256 * ((v >> 1) & 1) + 4 * (v >> 2));
-          R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
-        }
-        hex_coalesce_half(R);
-#else
-        const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 7u) + 16 * (lane >> 3));
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-          const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
-          R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
-        }
-        hex_coalesce(R, lane);
-#endif
-        if (a.skew != 0u) {
-          uint32_t e[4];
-          if (lane == 63u) {
-            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 8192));
-            e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
-            R[32 + i] = lane == 63u ? e[i] : nx;
-          }
-        }
-        return;
-      }
-    }
-    load_raw<NV>(a.in, a.skew, tb * gq, R);
-  };
-  if (first < a.units && whole(first)) load_unit_text(first);
+  auto load_text = [&](uint64_t gq) { load_unit_text<HEX>(a, gq, lane, R); };
+  if (first < a.units && whole(first)) load_text(first);
   for (uint64_t g = first; g < a.units; g += stride) {
     const uint64_t gn = g + stride;
     if (!whole(g)) {
       decode_unit_slow<HEX>(dec, a, g, pad, nout);
-      if (gn < a.units && whole(gn)) load_unit_text(gn);
+      if (gn < a.units && whole(gn)) load_text(gn);
       continue;
     }
     uint32_t T[16], bad = 0u;
@@ -1144,7 +1159,7 @@ __global__ void __launch_bounds__(256) decode_kernel(const AesArgs a) {
         for (int k = 0; k < 16; ++k) T[k] = tx[k];
       }
     }
-    if (gn < a.units && whole(gn)) load_unit_text(gn);  // next unit's text before the stores
+    if (gn < a.units && whole(gn)) load_text(gn);  // next unit's text before the stores
     uint32_t x[16], acc = 0u;
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = unb64_word(dec, T[k], acc);
@@ -1193,6 +1208,71 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) ctr_text_kernel(const 
         if (o < nout) a.out[o] = static_cast<uint8_t>(a.out[o] ^ (ks[k >> 2] >> (24 - 8 * (k & 3))));
       }
     }
+  }
+}
+
+// One pass again (DN_AES_DEC_SPLIT == 2): decode_kernel's coalesced,
+// transposed text reads (the next unit's loaded before this unit's AES) and
+// its decode, then the unit's three keystream blocks and one store of the
+// plaintext — no ciphertext round trip through HBM.
+template <int NR, bool HEX>
+__global__ void __launch_bounds__(1024) decrypt_fused_kernel(const AesArgs a) {
+  __shared__ AesLds<4> L;
+  build_tables<4>(L);
+  const uint32_t lb = (threadIdx.x & 31u) << 2;
+  const uint32_t lw[2] = {lb, lb | 0x10000u};
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 1024u;
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * 1024u + threadIdx.x;
+  uint32_t iv[4];
+  uint64_t pad;
+  text_header<HEX>(a, L.dec, iv, pad);
+  const uint64_t nout = a.n / 4 * 3 - pad - 16;
+  if (first == 0) *a.out_len = nout;
+  constexpr int NV = HEX ? 8 : 4;
+  uint32_t R[4 * NV + 4];
+  auto whole = [&](uint64_t g) { return g != 0 && g + 1 < a.units; };
+  const uint32_t lane = threadIdx.x & 63u;
+  if (first < a.units && whole(first)) load_unit_text<HEX>(a, first, lane, R);
+  for (uint64_t g = first; g < a.units; g += stride) {
+    const uint64_t gn = g + stride;
+    if (!whole(g)) {
+      decrypt_unit_slow<NR, 4, HEX>(L, lw, a, iv, g, pad, nout);
+      if (gn < a.units && whole(gn)) load_unit_text<HEX>(a, gn, lane, R);
+      continue;
+    }
+    uint32_t T[16], bad = 0u;
+    {
+      uint32_t tx[4 * NV];
+      shift_raw<NV>(R, a.skew, tx);
+      if constexpr (HEX) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[k] = pack_nibbles(unhex4(tx[2 * k], bad), unhex4(tx[2 * k + 1], bad));
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[k] = tx[k];
+      }
+    }
+    if (gn < a.units && whole(gn)) load_unit_text<HEX>(a, gn, lane, R);  // the next unit's text, ahead
+    uint32_t x[16], acc = 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = unb64_word(L.dec, T[k], acc);
+    if ((acc & (kDecPad | kDecBad)) | bad) atomicOr(a.bad, 1u);
+    uint32_t W[12];
+    join24(x, W);
+    uint32_t ks[3][4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) ctr_block(iv, 3 * g - 1 + j, ks[j]);
+#if DN_AES_DEC_NB == 3
+    aes_blocks<NR, 3>(L, lw, a, ks);
+#else
+#pragma unroll
+    for (int j = 0; j < 3; ++j) aes_block<NR>(L, lw, a, ks[j]);
+#endif
+    uint8_t* o = a.out + 48 * g - 16;  // plaintext bytes of keystream blocks 3g-1 .. 3g+1
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      store4(o + 16 * j, __builtin_bswap32(W[4 * j] ^ ks[j][0]), __builtin_bswap32(W[4 * j + 1] ^ ks[j][1]),
+             __builtin_bswap32(W[4 * j + 2] ^ ks[j][2]), __builtin_bswap32(W[4 * j + 3] ^ ks[j][3]));
   }
 }
 
@@ -1307,6 +1387,9 @@ static void launch(int kind, bool hex, uint64_t units, hipStream_t s, const AesA
   } else if (kind == kEncrypt) {
     if (hex) hipLaunchKernelGGL((encrypt_kernel<NR, NTAB, true>), g, b, 0, s, a);
     else hipLaunchKernelGGL((encrypt_kernel<NR, NTAB, false>), g, b, 0, s, a);
+  } else if (DN_AES_DEC_SPLIT == 2 && NTAB == 4) {
+    if (hex) hipLaunchKernelGGL((decrypt_fused_kernel<NR, true>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((decrypt_fused_kernel<NR, false>), g, b, 0, s, a);
   } else if (DN_AES_DEC_SPLIT) {
     // pass 1: decode, 256-thread workgroups; pass 2: CTR in place over the
     // ciphertext's 16-B blocks (at most units * 3 of them)
