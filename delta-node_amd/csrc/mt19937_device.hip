@@ -260,16 +260,36 @@ __device__ __forceinline__ void jump_mega(uint32_t (&Q)[11], const Lanes& L, con
   }
 }
 
+// DN_MT_JUMP_SMEM (default 1): a run's 11 words of g are read up front by
+// scalar loads (g is read-only for the kernel's lifetime: the constant
+// address space) — one wait per run, the chunk values extracted on the scalar
+// unit (~70 fewer VALU per step) — instead of a vector load per step whose
+// vmcnt(0) opened every step: the 2^24 level 171.6 vs 180.0 us on average,
+// make_shares_vec 2^20 -2 % (profiles/r05/y/).
+#ifndef DN_MT_JUMP_SMEM
+#define DN_MT_JUMP_SMEM 1
+#endif
+typedef __attribute__((address_space(4))) const uint64_t const_u64_t;
+
 template <int... ks>
 __device__ __forceinline__ void jump_run(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E,
                                          const uint32_t (&off)[16], const uint64_t* g, int wi, int top,
                                          std::integer_sequence<int, ks...>) {
+#if DN_MT_JUMP_SMEM
+  const_u64_t* gc = (const_u64_t*)(g);
+  const int tu = __builtin_amdgcn_readfirstlane(top);
+  uint64_t gws[sizeof...(ks)];
+  ((void)(gws[ks] = gc[__builtin_amdgcn_readfirstlane(wi - ks <= tu ? wi - ks : tu)]), ...);  // in range
+  ((void)(gws[ks] = (wi - ks) <= tu ? gws[ks] : 0ull), ...);
+  ((void)jump_mega<ks>(Q, L, E, off, gws[ks]), ...);
+#else
   ((void)[&] {
      const int w = wi - ks;
      const uint64_t gw = w <= top ? g[w] : 0ull;
      jump_mega<ks>(Q, L, E, off, gw);
    }(),
    ...);
+#endif
 }
 
 // One workgroup = up to W jumps (or parts of jumps, words [lo, hi) of g)
@@ -387,6 +407,7 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   }
   int top = hi - 1;
   while (top > lo && g[top] == 0ull) --top;  // steps above it leave r = 0
+  top = __builtin_amdgcn_readfirstlane(top);
   // runs of 11 steps (the frame returns to Q[0] after 11) ending at word lo;
   // r = 0 before the first nonzero word, so a run starts with zero words above it
   if (a.probe != 1u)
