@@ -195,3 +195,35 @@ def test_vector_share_envelope_roundtrip():
     recs = aes.decrypt_vec(key, env, hex=True)
     vec, xs = codec.decode_share_vec(recs, offs, N)
     assert torch.equal(vec, block[1]) and bool((xs == 2).all())
+
+
+def test_bad_characters_inside_full_waves():
+    """A bad character in the middle of a long text — where the decrypt reads
+    whole waves of units line by line (decrypt_fused_kernel) — is flagged, and
+    the call then behaves as the reference's own calls do (aes.py:17-23,
+    hex.py:29-41)."""
+    key, nonce = KEYS[0], NONCES[2]
+    data = rand_bytes(300_000, 77)
+    b64 = want_text(key, nonce, data)
+    mid = len(b64) // 2 + 5
+    for bad in (b"*", b"=", b"\n", b"-"):
+        t64 = b64[:mid] + bad + b64[mid + 1:]
+        for hex_ in (False, True):
+            t = (b"0x" + t64.hex().encode()) if hex_ else t64
+            try:
+                want = ref_decrypt(key, t, hex_)
+            except ValueError as e:
+                with pytest.raises(type(e)):
+                    aes.decrypt_vec(key, to_dev(t), hex=hex_)
+                continue
+            assert host(aes.decrypt_vec(key, to_dev(t), hex=hex_)) == want, (bad, hex_)
+    hx = want_text(key, nonce, data, True)
+    for bad in (b"g", b" ", b"\x80"):
+        t = hx[:2 + 2 * mid] + bad + hx[3 + 2 * mid:]
+        try:
+            want = ref_decrypt(key, t, True)
+        except ValueError:  # fromhex / the ascii decode refuse it
+            with pytest.raises(ValueError):
+                aes.decrypt_vec(key, to_dev(t), hex=True)
+            continue
+        assert host(aes.decrypt_vec(key, to_dev(t), hex=True)) == want, bad
