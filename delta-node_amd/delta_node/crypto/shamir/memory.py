@@ -65,7 +65,11 @@ POOL_IDLE_BYTES = 32 << 30     # most idle bytes the pool keeps mapped
 POOL_MIN_FREE = 16 << 30       # device bytes kept free beside the idle blocks
 PROBE_MIN_BYTES = 64 << 20     # new share blocks from this size up are write-rate probed (every chunked one)
 PROBE_TRIES = 4                # most blocks mapped for one request (blocks of 1 GiB or more)
-PROBE_TRIES_SMALL = 12         # ... for smaller blocks (a try maps a few chunks and writes for microseconds)
+# ... for smaller blocks (a try maps a few chunks and writes for microseconds;
+# within PROBE_BUDGET): a 2^21 shard's block took the best of 12 slow tries on
+# some boxes, 48 found a fast one (bench --log2n 21: 8.58-8.60 vs 8.46-8.49e9
+# elements/s, profiles/r05/ac/)
+PROBE_TRIES_SMALL = 48
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
 PROBE_FAST = 6.8e12            # the first block of a class keeps at once at this tiled-probe rate (B/s)
 PROBE_BUDGET = 24 << 30        # most bytes mapped at once for one request's tries
