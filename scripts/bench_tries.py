@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""bench.py with memory.PROBE_TRIES_SMALL set to argv[1] (an A/B of the probe's
-tries for share blocks under 1 GiB); the remaining arguments go to bench.py."""
+"""bench.py with the share-block probe's tries set from argv[1] (an A/B of the
+probe policy, memory.py): "SMALL" or "SMALL,LARGE,BUDGET_GIB" sets
+PROBE_TRIES_SMALL (blocks under 1 GiB), PROBE_TRIES (1 GiB and up) and
+PROBE_BUDGET; the remaining arguments go to bench.py."""
 import os
 import runpy
 import sys
@@ -9,6 +11,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "delta-node_amd"))
 from delta_node.crypto.shamir import memory  # noqa: E402
 
-memory.PROBE_TRIES_SMALL = int(sys.argv[1])
+vals = [int(v) for v in sys.argv[1].split(",")]
+memory.PROBE_TRIES_SMALL = vals[0]
+if len(vals) > 1:
+    memory.PROBE_TRIES = vals[1]
+    memory.PROBE_BUDGET = vals[2] << 30
 sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[2:]
 runpy.run_path(sys.argv[0], run_name="__main__")
