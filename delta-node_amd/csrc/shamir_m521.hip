@@ -486,13 +486,89 @@ struct ReconArgs {
 // small odd d) and by 2^shift (a 521-bit rotation).
 // K > 0: compile-time share count — all K*17 loads of an element are issued
 // before the first multiply; K == 0: runtime count, one share at a time.
+// S reduced, divided and stored for element w of the tile; returns whether
+// the result is >= 2^64 (the overflow count).
+template <int A, int INV>
+__device__ __forceinline__ bool recon_finish(const ReconArgs& a, uint32_t tile, uint32_t w,
+                                             uint32_t (&S)[A + kLimbs]) {
+  constexpr int N = A + kLimbs;
+  constexpr int VB = (A == kLimbs) ? 1046 : (521 + 32 * A + 4);
+  uint32_t r[kLimbs];
+  reduce_wide<N, VB>(S, r);
+  if constexpr (INV == 1) {
+    uint32_t t[kLimbs];
+    mulmod(t, r, a.inv);
+#pragma unroll
+    for (int l = 0; l < kLimbs; ++l) r[l] = t[l];
+  } else if constexpr (INV == 2) {
+    exact_div_small(r, a.d, a.d_inv32, a.p_inv_d, a.d_recip, a.w);
+  }
+  if (a.shift != 0u) rotr521(r, a.shift);
+  if (a.out_fe) store_fe(tile_base(a.out_fe, tile), w, r);
+  if (a.out_u64) {
+    const uint64_t lo = static_cast<uint64_t>(r[0]) | (static_cast<uint64_t>(r[1]) << 32);
+    __builtin_nontemporal_store(static_cast<int64_t>(lo), a.out_u64 + static_cast<uint64_t>(tile) * kTile + w);
+  }
+  uint32_t hi_or = 0u;
+#pragma unroll
+  for (int l = 2; l < kLimbs; ++l) hi_or |= r[l];
+  return hi_or != 0u;
+}
+
+// One element's S from its K loaded rows (K > 0), then recon_finish.
+template <int A, int INV, int K>
+__device__ __forceinline__ bool recon_rows(const ReconArgs& a, uint32_t tile, uint32_t w, uint32_t (&y)[K][kLimbs]) {
+  uint32_t S[A + kLimbs];
+#pragma unroll
+  for (int i = 0; i < A + kLimbs; ++i) S[i] = 0u;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    if ((a.neg >> i) & 1u) {  // -y == p - y == ~y within 521 bits
+#pragma unroll
+      for (int l = 0; l < 16; ++l) y[i][l] = ~y[i][l];
+      y[i][16] = (~y[i][16]) & kTopMask;
+    }
+    mac_wide<A + kLimbs, A>(S, a.a[i], y[i]);
+  }
+  return recon_finish<A, INV>(a, tile, w, S);
+}
+
+// DN_RECON_PF (default 1): a wave working a whole tile's four quarters loads
+// quarter q + 1's K rows before quarter q's arithmetic (164 VGPRs for K = 3,
+// 3 waves per SIMD; capping it at 4 or 5 spills): the headline reconstruct
+// 0.599-0.603 vs 0.611-0.616 ms (profiles/r05/ai/).
+#ifndef DN_RECON_PF
+#define DN_RECON_PF 1
+#endif
+
 template <int A, int INV, int K>
 __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) {
   constexpr int N = A + kLimbs;
-  constexpr int VB = (A == kLimbs) ? 1046 : (521 + 32 * A + 4);
   const uint32_t lane = threadIdx.x & 63u;
   const WaveSched ws = wave_sched(a.tile_map, a.ntiles);
   for (uint32_t tile = ws.first; tile < ws.end; tile += ws.step) {
+#if DN_RECON_PF
+    if constexpr (K > 0) {
+      if (ws.q0 == 0u && ws.q1 == 4u && (static_cast<uint64_t>(tile) + 1u) * kTile <= a.n_elem) {
+        uint32_t y[2][K][kLimbs];
+#pragma unroll
+        for (int i = 0; i < K; ++i) load_fe(tile_base(a.shares[i], tile), lane, y[0][i]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q < 3) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) load_fe(tile_base(a.shares[i], tile), lane + 64u * (q + 1), y[(q + 1) & 1][i]);
+          }
+          const bool over = recon_rows<A, INV, K>(a, tile, lane + 64u * q, y[q & 1]);
+          if (a.overflow) {
+            const uint64_t m = __ballot(over);
+            if (lane == 0 && m) atomicAdd(a.overflow, static_cast<uint32_t>(__popcll(m)));
+          }
+        }
+        continue;
+      }
+    }
+#endif
 #pragma unroll 1
     for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
@@ -500,23 +576,15 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
       const bool valid = e < a.n_elem;
       bool over = false;
       if (valid) {
-        uint32_t S[N];
-#pragma unroll
-        for (int i = 0; i < N; ++i) S[i] = 0u;
         if constexpr (K > 0) {
           uint32_t y[K][kLimbs];
 #pragma unroll
           for (int i = 0; i < K; ++i) load_fe(tile_base(a.shares[i], tile), w, y[i]);
-#pragma unroll
-          for (int i = 0; i < K; ++i) {
-            if ((a.neg >> i) & 1u) {  // -y == p - y == ~y within 521 bits
-#pragma unroll
-              for (int l = 0; l < 16; ++l) y[i][l] = ~y[i][l];
-              y[i][16] = (~y[i][16]) & kTopMask;
-            }
-            mac_wide<N, A>(S, a.a[i], y[i]);
-          }
+          over = recon_rows<A, INV, K>(a, tile, w, y);
         } else {
+          uint32_t S[N];
+#pragma unroll
+          for (int i = 0; i < N; ++i) S[i] = 0u;
 #pragma unroll 1
           for (int32_t i = 0; i < a.k; ++i) {
             uint32_t y[kLimbs];
@@ -528,27 +596,8 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
             }
             mac_wide<N, A>(S, a.a[i], y);
           }
+          over = recon_finish<A, INV>(a, tile, w, S);
         }
-        uint32_t r[kLimbs];
-        reduce_wide<N, VB>(S, r);
-        if constexpr (INV == 1) {
-          uint32_t t[kLimbs];
-          mulmod(t, r, a.inv);
-#pragma unroll
-          for (int l = 0; l < kLimbs; ++l) r[l] = t[l];
-        } else if constexpr (INV == 2) {
-          exact_div_small(r, a.d, a.d_inv32, a.p_inv_d, a.d_recip, a.w);
-        }
-        if (a.shift != 0u) rotr521(r, a.shift);
-        if (a.out_fe) store_fe(tile_base(a.out_fe, tile), w, r);
-        if (a.out_u64) {
-          const uint64_t lo = static_cast<uint64_t>(r[0]) | (static_cast<uint64_t>(r[1]) << 32);
-          __builtin_nontemporal_store(static_cast<int64_t>(lo), a.out_u64 + static_cast<uint64_t>(tile) * kTile + w);
-        }
-        uint32_t hi_or = 0u;
-#pragma unroll
-        for (int l = 2; l < kLimbs; ++l) hi_or |= r[l];
-        over = hi_or != 0u;
       }
       if (a.overflow) {
         const uint64_t m = __ballot(over);

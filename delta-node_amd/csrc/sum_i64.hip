@@ -23,14 +23,33 @@ struct SumArgs {
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
+// DN_SUM_WIDE: 16-B pairs per lane and step, each a wave's width (64 pairs,
+// 1 KB) further on, all loads of a step issued before the adds — a wave reads
+// 8 KB of each member per step: at 10 x 2^24, 8 (default) 0.227-0.229 ms, 4
+// 0.231, 2 0.236-0.238, 1 0.258-0.265 (0.80 vs 0.71 of 8 TB/s;
+// profiles/r05/ae/, af/, ah/)
+#ifndef DN_SUM_WIDE
+#define DN_SUM_WIDE 8
+#endif
 __global__ void __launch_bounds__(256) i64_sum_kernel(const SumArgs a) {
+  constexpr int V = DN_SUM_WIDE;
   const uint64_t pairs = a.n / 2;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < pairs; i += stride) {
-    u64x2 acc = {0, 0};
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x * V;
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * blockDim.x * V + (threadIdx.x & ~63u) * V + (threadIdx.x & 63u);
+  for (uint64_t i = first; i < pairs; i += stride) {
+    u64x2 acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = u64x2{0, 0};
 #pragma unroll 4
-    for (int j = 0; j < a.k; ++j) acc += __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(a.in[j]) + i);
-    __builtin_nontemporal_store(acc, reinterpret_cast<u64x2*>(a.out) + i);
+    for (int j = 0; j < a.k; ++j) {
+      const u64x2* p = reinterpret_cast<const u64x2*>(a.in[j]) + i;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        if (i + 64 * v < pairs) acc[v] += __builtin_nontemporal_load(p + 64 * v);
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      if (i + 64 * v < pairs) __builtin_nontemporal_store(acc[v], reinterpret_cast<u64x2*>(a.out) + i + 64 * v);
   }
   if ((a.n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     uint64_t acc = 0;
