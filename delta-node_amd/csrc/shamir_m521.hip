@@ -167,6 +167,13 @@ __device__ __forceinline__ void prng_coeffs_of(const SplitArgs& a, uint32_t tile
 
 constexpr int kMaxPrngT = 8;
 
+// DN_SPLIT_PF (variant builds): the next quarter's loads ahead of the current
+// quarter's stores (explicit coefficients, difference table) — neutral to
+// 1 % slower on the headline (9.06-9.13 vs 9.10-9.18e9 elements/s,
+// profiles/r05/aj/): the split already runs at ~0.97 of its ceiling
+#ifndef DN_SPLIT_PF
+#define DN_SPLIT_PF 0
+#endif
 template <int T, bool FE_SECRET, bool FOLD, bool PRNG, int SAUX>
 __device__ __forceinline__ void split_body(const SplitArgs& a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -182,6 +189,36 @@ __device__ __forceinline__ void split_body(const SplitArgs& a) {
     for (int k = 0; k < TP; ++k) {
     const uint32_t tile = tile0 + static_cast<uint32_t>(k) * ws.step;
     if (tile >= ws.end) break;
+#if DN_SPLIT_PF
+    if constexpr (!PRNG && !FOLD) {
+      // a whole tile's four quarters: quarter q + 1's coefficients and secret
+      // loaded before quarter q's share stores
+      if (ws.q0 == 0u && ws.q1 == 4u && (static_cast<uint64_t>(tile) + 1u) * kTile <= a.n_elem) {
+        uint32_t cq[2][T][kLimbs];
+        auto load_q = [&](uint32_t w, uint32_t (&cc)[T][kLimbs]) {
+#pragma unroll
+          for (int j = 1; j < T; ++j)
+            load_fe_b(tile_rsrc(tile_base(a.coeffs + static_cast<uint64_t>(j - 1) * a.coeff_stride, tile)), w, cc[j]);
+          load_secret<FE_SECRET>(a, tile, w, cc[0]);
+        };
+        load_q(lane, cq[0]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q < 3) load_q(lane + 64u * static_cast<uint32_t>(q + 1), cq[(q + 1) & 1]);
+          const uint32_t w = lane + 64u * static_cast<uint32_t>(q);
+          uint32_t (&D)[T][kLimbs] = cq[q & 1];
+          fd_init<T>(D);
+#pragma unroll 1
+          for (int32_t xi = 1; xi <= a.n_shares; ++xi) {
+            store_reduced<SAUX>(tile_rsrc(tile_base(a.shares + static_cast<uint64_t>(xi - 1) * a.share_stride, tile)),
+                                w, D[0]);
+            fd_step<T>(D);
+          }
+        }
+        continue;
+      }
+    }
+#endif
 #pragma unroll 1
     for (uint32_t q = ws.q0; q < ws.q1; ++q) {
       const uint32_t w = lane + 64u * q;
