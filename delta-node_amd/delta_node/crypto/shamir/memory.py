@@ -64,7 +64,12 @@ CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
 POOL_IDLE_BYTES = 32 << 30     # most idle bytes the pool keeps mapped
 POOL_MIN_FREE = 16 << 30       # device bytes kept free beside the idle blocks
 PROBE_MIN_BYTES = 64 << 20     # new share blocks from this size up are write-rate probed (every chunked one)
-PROBE_TRIES = 4                # most blocks mapped for one request (blocks of 1 GiB or more)
+# most blocks mapped for one request (blocks of 1 GiB or more); a request
+# stops at the first block close to the best rate, so more tries are spent
+# only where the memory handed out is slow: one box's fifth 5.5 GB block was
+# the best of 4 slow tries (5.8 TB/s, its split 1.52 ms against 1.26-1.29;
+# profiles/r05/final4/)
+PROBE_TRIES = 8
 # ... for smaller blocks (a try maps a few chunks and writes for microseconds;
 # within PROBE_BUDGET): a 2^21 shard's block took the best of 12 slow tries on
 # some boxes, 48 found a fast one (bench --log2n 21: 8.58-8.60 vs 8.46-8.49e9
@@ -72,7 +77,8 @@ PROBE_TRIES = 4                # most blocks mapped for one request (blocks of 1
 PROBE_TRIES_SMALL = 48
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
 PROBE_FAST = 6.8e12            # the first block of a class keeps at once at this tiled-probe rate (B/s)
-PROBE_BUDGET = 24 << 30        # most bytes mapped at once for one request's tries
+PROBE_BUDGET = 48 << 30        # most bytes mapped at once for one request's tries (and
+                               # never more than the device has free beyond POOL_MIN_FREE)
 
 _lock = threading.RLock()
 _idle: Dict[Tuple[int, int, int], List[Tuple[int, int]]] = {}  # (device, nbytes, chunk) -> [(age, ptr)]
@@ -275,7 +281,8 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
     tiled = len(shape) == 2 and int(shape[0]) > 0 and int(shape[1]) % field.TILE_BYTES == 0
     cands: List[Tuple[float, int]] = []
     most = PROBE_TRIES if nbytes >= (1 << 30) else PROBE_TRIES_SMALL
-    tries = max(1, min(most, PROBE_BUDGET // max(1, nbytes)))
+    spare = max(0, _mem_info(dev.index)[0] - POOL_MIN_FREE)  # torch keeps its margin
+    tries = max(1, min(most, PROBE_BUDGET // max(1, nbytes), spare // max(1, nbytes)))
     for k in range(tries):
         try:
             ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)

@@ -41,6 +41,7 @@ def fake(monkeypatch):
         monkeypatch.setattr(memory, "_best_rate", {})
         monkeypatch.setattr(memory, "_rates", {})
         monkeypatch.setattr(memory, "_current_stream", lambda index: 0)
+        monkeypatch.setattr(memory, "_mem_info", lambda index: (1 << 50, 1 << 50))
         return f
     return make
 
@@ -85,12 +86,21 @@ NBIG = BIG[0] * BIG[1]
 
 
 def test_slow_block_redrawn_up_to_the_try_limit(fake):
-    f = fake([7.0, 6.0, 5.0, 5.5, 6.5, 5.2, 9.9])
+    slow = [5.0, 5.5, 6.5] + [5.2] * (memory.PROBE_TRIES - 3)
+    f = fake([7.0, 6.0] + slow + [9.9])
     memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # keeps 7.0, frees 6.0
-    p = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # 5.0, 5.5, 6.5, 5.2: none close, keeps 6.5
+    p = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # PROBE_TRIES tries, none close: keeps 6.5
     assert f.rate_of[p] == 6.5
-    assert sorted(f.rate_of[q] for q in f.freed) == [5.0, 5.2, 5.5, 6.0]
+    assert sorted(f.rate_of[q] for q in f.freed) == sorted([6.0] + [r for r in slow if r != 6.5])
     assert f.rates == [9.9]  # PROBE_TRIES blocks at most
+
+
+def test_tries_bounded_by_free_memory(fake, monkeypatch):
+    f = fake([7.0, 6.0, 5.0, 5.5, 6.5, 9.9])
+    memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # keeps 7.0, frees 6.0
+    monkeypatch.setattr(memory, "_mem_info", lambda index: (memory.POOL_MIN_FREE + 2 * NBIG + 1, 288 << 30))
+    p = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # room for two tries beyond the margin
+    assert f.rate_of[p] == 5.5 and f.rates == [6.5, 9.9]
 
 
 def test_small_blocks_get_more_tries(fake):
