@@ -76,6 +76,14 @@ PROBE_TRIES = 8
 # elements/s, profiles/r05/ac/)
 PROBE_TRIES_SMALL = 48
 PROBE_KEEP = 0.96              # fraction of the best rate seen that a block must reach
+# the first block of a class (no rate to compare with yet): the fastest of this
+# many tries — 2 from 1 GiB up (each try maps and writes gigabytes: the cold
+# first call), 4 below (a 2^21 shard's first 692 MB block was the best of two
+# at 5.7-5.9 TB/s while its later blocks reached 6.2-6.7, profiles/r05/ak/;
+# best of 4: the 2^21 line 8.78-8.85 vs 8.76-8.81e9 elements/s, its split
+# 0.159-0.162 vs 0.163-0.164 ms, at up to ~70 probes once, profiles/r05/al/)
+PROBE_FIRST = 2
+PROBE_FIRST_SMALL = 4
 PROBE_FAST = 6.8e12            # the first block of a class keeps at once at this tiled-probe rate (B/s)
 PROBE_BUDGET = 48 << 30        # most bytes mapped at once for one request's tries (and
                                # never more than the device has free beyond POOL_MIN_FREE)
@@ -281,6 +289,7 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
     tiled = len(shape) == 2 and int(shape[0]) > 0 and int(shape[1]) % field.TILE_BYTES == 0
     cands: List[Tuple[float, int]] = []
     most = PROBE_TRIES if nbytes >= (1 << 30) else PROBE_TRIES_SMALL
+    first = PROBE_FIRST if nbytes >= (1 << 30) else PROBE_FIRST_SMALL
     spare = max(0, _mem_info(dev.index)[0] - POOL_MIN_FREE)  # torch keeps its margin
     tries = max(1, min(most, PROBE_BUDGET // max(1, nbytes), spare // max(1, nbytes)))
     for k in range(tries):
@@ -296,7 +305,7 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
         if best is None and tiled and rate >= PROBE_FAST:  # the class's first block, in the fast class
             break
         if best is None:
-            if k >= 1:  # the first large block of its class on this device: the faster of two
+            if k >= first - 1:  # the class's first block on this device: the fastest of `first`
                 break
         elif rate >= PROBE_KEEP * best:
             break

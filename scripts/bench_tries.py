@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """bench.py with the share-block probe's tries set from argv[1] (an A/B of the
-probe policy, memory.py): "SMALL" or "SMALL,LARGE,BUDGET_GIB" sets
-PROBE_TRIES_SMALL (blocks under 1 GiB), PROBE_TRIES (1 GiB and up) and
-PROBE_BUDGET; the remaining arguments go to bench.py."""
+probe policy, memory.py): "SMALL" or "SMALL,LARGE,BUDGET_GIB[,FIRST_SMALL]"
+sets PROBE_TRIES_SMALL (blocks under 1 GiB), PROBE_TRIES (1 GiB and up),
+PROBE_BUDGET and PROBE_FIRST_SMALL; the remaining arguments go to bench.py."""
 import os
 import runpy
 import sys
@@ -16,5 +16,7 @@ memory.PROBE_TRIES_SMALL = vals[0]
 if len(vals) > 1:
     memory.PROBE_TRIES = vals[1]
     memory.PROBE_BUDGET = vals[2] << 30
+if len(vals) > 3:
+    memory.PROBE_FIRST_SMALL = vals[3]
 sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[2:]
 runpy.run_path(sys.argv[0], run_name="__main__")

@@ -42,6 +42,7 @@ def fake(monkeypatch):
         monkeypatch.setattr(memory, "_rates", {})
         monkeypatch.setattr(memory, "_current_stream", lambda index: 0)
         monkeypatch.setattr(memory, "_mem_info", lambda index: (1 << 50, 1 << 50))
+        monkeypatch.setattr(memory, "PROBE_FIRST_SMALL", 2)  # the tests below script two first tries
         return f
     return make
 
@@ -263,3 +264,13 @@ def test_record_stream_adds_a_stream_to_the_live_block(pool):
     outside = types.SimpleNamespace(data_ptr=lambda: 0x1000 + KEY[1])
     memory.record_stream(outside, 12)
     assert b.streams == {7, 11}
+
+
+def test_first_small_block_is_the_fastest_of_probe_first_small(fake, monkeypatch):
+    f = fake([5.0, 7.0, 6.0, 7.5, 9.0])
+    monkeypatch.setattr(memory, "PROBE_FIRST_SMALL", 4)
+    p = memory._alloc_probed(NB, 2 << 20, DEV, SHAPE)  # under 1 GiB: the fastest of four
+    assert f.rate_of[p] == 7.5 and len(f.freed) == 3 and f.rates == [9.0]
+    g = fake([5.0, 7.0, 9.0])
+    q = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # 1 GiB and up: the faster of PROBE_FIRST = 2
+    assert g.rate_of[q] == 7.0 and g.rates == [9.0]
