@@ -4,8 +4,8 @@ The split writes 330 B per element at 3-of-5 (70 % of its traffic) and its
 rate follows the physical pages of the share block: a 5.5 GB
 block from one hipMalloc lands in a fast or a slow class (0.66 / 0.78 of
 8 TB/s for the split).  A block built from physical chunks (CHUNK_BYTES)
-mapped back to back (hipMemCreate / hipMemMap) ran in the fast class every time it was
-measured — 10 of 10 blocks at 0.786-0.800 against 6 of 10 torch.empty blocks
+mapped back to back (hipMemCreate / hipMemMap) ran in the fast class every
+time it was measured — 10 of 10 blocks at 0.786-0.800 against 6 of 10 torch.empty blocks
 (profiles/r04/a/block_probe.jsonl, and round 1's place_vmm2/3) — so the vector
 API allocates the share blocks it returns here (`share_block`), and callers
 may too.  Every API keeps accepting tensors from any allocator.
@@ -40,10 +40,12 @@ profiles/r04/q/block_class.jsonl).  So a NEW share block of at least
 per tile, every row's slice) and kept only if it writes
 at >= `PROBE_KEEP` of the best rate this process has seen on the device
 for blocks of that many rows and that size class (log2 of the bytes);
-otherwise up to `PROBE_TRIES` blocks (at most `PROBE_BUDGET` bytes of them)
-are mapped and the fastest is kept (the others are freed after the choice, so
-a retry cannot get their pages back).
-The first large block on a device is the faster of two.
+otherwise up to `PROBE_TRIES` blocks (`PROBE_TRIES_SMALL` under 1 GiB; at
+most `PROBE_BUDGET` bytes of them, within the device's free memory) are
+mapped and the fastest is kept (the others are freed after the choice, so a
+retry cannot get their pages back).  The first block of a class on a device
+is the fastest of `PROBE_FIRST` (`PROBE_FIRST_SMALL` under 1 GiB) tries, or
+the first to reach `PROBE_FAST`.
 """
 from __future__ import annotations
 
