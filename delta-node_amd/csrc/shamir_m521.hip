@@ -571,9 +571,10 @@ __device__ __forceinline__ bool recon_rows(const ReconArgs& a, uint32_t tile, ui
 }
 
 // DN_RECON_PF (default 1): a wave working a whole tile's four quarters loads
-// quarter q + 1's K rows before quarter q's arithmetic (164 VGPRs for K = 3,
+// quarter q + DN_RECON_PF's K rows before quarter q's arithmetic (164 VGPRs for K = 3,
 // 3 waves per SIMD; capping it at 4 or 5 spills): the headline reconstruct
-// 0.599-0.603 vs 0.611-0.616 ms (profiles/r05/ai/).
+// 0.599-0.603 vs 0.611-0.616 ms (profiles/r05/ai/); two quarters ahead (212
+// VGPRs) the same, 0.585-0.589 vs 0.564-0.591 ms (profiles/r05/an/).
 #ifndef DN_RECON_PF
 #define DN_RECON_PF 1
 #endif
@@ -587,16 +588,20 @@ __global__ void __launch_bounds__(kBlock) reconstruct_kernel(const ReconArgs a) 
 #if DN_RECON_PF
     if constexpr (K > 0) {
       if (ws.q0 == 0u && ws.q1 == 4u && (static_cast<uint64_t>(tile) + 1u) * kTile <= a.n_elem) {
-        uint32_t y[2][K][kLimbs];
+        constexpr int D = DN_RECON_PF, B = D + 1;  // quarters loaded ahead, buffers
+        uint32_t y[B][K][kLimbs];
 #pragma unroll
-        for (int i = 0; i < K; ++i) load_fe(tile_base(a.shares[i], tile), lane, y[0][i]);
+        for (int p = 0; p < D; ++p)
+#pragma unroll
+          for (int i = 0; i < K; ++i) load_fe(tile_base(a.shares[i], tile), lane + 64u * p, y[p % B][i]);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          if (q < 3) {
+          if (q + D < 4) {
 #pragma unroll
-            for (int i = 0; i < K; ++i) load_fe(tile_base(a.shares[i], tile), lane + 64u * (q + 1), y[(q + 1) & 1][i]);
+            for (int i = 0; i < K; ++i)
+              load_fe(tile_base(a.shares[i], tile), lane + 64u * (q + D), y[(q + D) % B][i]);
           }
-          const bool over = recon_rows<A, INV, K>(a, tile, lane + 64u * q, y[q & 1]);
+          const bool over = recon_rows<A, INV, K>(a, tile, lane + 64u * q, y[q % B]);
           if (a.overflow) {
             const uint64_t m = __ballot(over);
             if (lane == 0 && m) atomicAdd(a.overflow, static_cast<uint32_t>(__popcll(m)));
