@@ -206,6 +206,35 @@ def c_port_baseline(t: int, n: int, xs, budget_s: float, threads: int) -> dict:
                       f"n={n} + reconstruct xs={list(xs)}), C restatement, {wall:.1f} s wall"}
 
 
+def caller_blocks_row(sec, coeffs, N: int, t: int, n: int, nblocks: int, stream, split_bytes: int, want,
+                      reps: int = 4) -> dict:
+    """The headline split on share blocks a caller allocates itself
+    (torch.empty, the C-ABI's caller-owned memory, dn_shamir.h): the same
+    kernel and inputs as the timed steps, `nblocks` separately allocated
+    blocks, the mean of `reps` launches on each after a first touch — what a
+    caller passing its own `out` gets, beside the probed pool blocks."""
+    from delta_node.crypto.shamir import _native
+
+    blocks = [torch.empty((n, want.shape[1]), dtype=torch.uint8, device=sec.device) for _ in range(nblocks)]
+    ms = []
+    for b in blocks:
+        _native.split_u64(sec, coeffs, b, N, t, n)
+        evs = [(TimingEvent(), TimingEvent()) for _ in range(reps)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            _native.split_u64(sec, coeffs, b, N, t, n)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        ms.append(float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs])))
+    equal = all(bool(torch.equal(b, want)) for b in blocks)
+    del blocks
+    fr = [split_bytes / (m * 1e-3) / 1e9 / PEAK_HBM_GBPS for m in ms]
+    return {"allocator": "torch.empty (one hipMalloc each, not probed)", "blocks": nblocks,
+            "launches_per_block": reps, "split_ms": ms, "frac": fr, "frac_min": min(fr),
+            "frac_median": float(np.median(fr)), "frac_max": max(fr), "frac_mean_time": split_bytes / (
+                float(np.mean(ms)) * 1e-3) / 1e9 / PEAK_HBM_GBPS, "equal_to_timed_block": equal}
+
+
 def stream_ceiling(ins, in_bpt, outs, out_bpt, ntiles: int, reps: int = 5) -> dict:
     """dn_diag_tile_stream (lib/libdn_diag.so): per tile, 16-B non-temporal
     loads of `in_bpt[i]` bytes from every input buffer, then 16-B stores of
@@ -425,7 +454,19 @@ def envelope_row(recs, reps: int, s, e) -> dict:
         env = aes.encrypt_vec(key, recs, nonce=nonce, hex=True)
     e.record()
     torch.cuda.synchronize()
+    enc_alloc_ms = s.elapsed_time(e) / reps
+    # the API call on a reused buffer (encrypt_buffer): the kernel + one 2-byte "0x" copy
+    obuf = aes.encrypt_buffer(n, True, recs.device)
+    env2 = aes.encrypt_vec(key, recs, nonce=nonce, hex=True, out=obuf)
+    warm(lambda: aes.encrypt_vec(key, recs, nonce=nonce, hex=True, out=obuf))
+    s.record()
+    for _ in range(reps):
+        env2 = aes.encrypt_vec(key, recs, nonce=nonce, hex=True, out=obuf)
+    e.record()
+    torch.cuda.synchronize()
     enc_ms = s.elapsed_time(e) / reps
+    out_equal = bool(torch.equal(env2, env))
+    del env2, obuf
     back = aes.decrypt_vec(key, env, hex=True)
     torch.cuda.synchronize()
     s.record()
@@ -492,12 +533,15 @@ def envelope_row(recs, reps: int, s, e) -> dict:
     lds_bytes = (n + 15) // 16 * 14 * 16 * 4
     row = {"workload": f"packed records of share x=3 ({n / 1e9:.2f} GB) <-> '0x' + hex(base64(nonce || AES-256-CTR)) "
                        f"({text_bytes / 1e9:.2f} GB)",
-           "encrypt_ms": enc_ms, "decrypt_ms": dec_ms,
+           "encrypt_ms": enc_ms, "decrypt_ms": dec_ms, "encrypt_alloc_ms": enc_alloc_ms,
+           "encrypt_over_kernel": enc_ms / enc_kernel_ms, "encrypt_out_equal": out_equal,
            "encrypt_kernel_ms": enc_kernel_ms, "encrypt_kernel_equal_api": kernel_equal,
            "decrypt_kernel_ms": dec_kernel_ms, "decrypt_kernel_roundtrip": dec_kernel_equal,
-           "timing": "encrypt_ms / decrypt_ms: the Python API calls (output allocation, decrypt's length "
-                     "read-back), mean of one round; encrypt_kernel_ms: dn_aes_encrypt on a preallocated "
-                     "buffer, >= 0.15 s warm-up, best of 3 rounds; the rooflines use the kernel time",
+           "timing": "encrypt_ms: the Python API call on a reused buffer (out=encrypt_buffer(n, hex)), "
+                     "after >= 0.15 s of warm-up; encrypt_alloc_ms: the API call allocating its 3 GB output; "
+                     "decrypt_ms: the API call (output allocation, the length read-back), mean of one round; "
+                     "encrypt_kernel_ms: dn_aes_encrypt on a preallocated buffer, >= 0.15 s warm-up, best of "
+                     "3 rounds; the rooflines use the kernel time",
            "encrypt_plaintext_GBps": n / (enc_ms * 1e-3) / 1e9, "decrypt_plaintext_GBps": n / (dec_ms * 1e-3) / 1e9,
            "roofline_lds": roof("lds", lds_bytes / (enc_kernel_ms * 1e-3) / 1e9,
                                 "14 rounds x 16 Te lookups x 4 B per 16-byte block (encrypt kernel)"),
@@ -617,20 +661,43 @@ def rows_bench(dev, log2n: int) -> dict:
     blk = ss.make_shares_vec(torch.from_numpy(secrets_int64(3, n)), 5)
     packed, offs = codec.encode_share_vec(blk[2], n, 3)
     torch.cuda.synchronize()
-    # the API calls (allocation of the outputs, the decoder's bad-record read-back included)
+    # the API calls: allocating their outputs (the decoder's bad-record
+    # read-back per call) and on caller buffers (the decoder's check deferred
+    # to one read-back after the loop: decode_share_vec(..., bad=flag))
     s.record()
     for _ in range(reps):
         packed, offs = codec.encode_share_vec(blk[2], n, 3, trim=False)
     e.record()
     torch.cuda.synchronize()
-    enc_call_ms = s.elapsed_time(e) / reps
+    enc_alloc_ms = s.elapsed_time(e) / reps
     total = int(offs[n].item())
     s.record()
     for _ in range(reps):
         vec, _xs = codec.decode_share_vec(packed, offs, n)
     e.record()
     torch.cuda.synchronize()
+    dec_alloc_ms = s.elapsed_time(e) / reps
+    cpk, cof = torch.empty_like(packed), torch.empty_like(offs)
+    cvec, cxs = torch.empty_like(vec), torch.empty(n, dtype=torch.int64, device=dev)
+    cbad = torch.zeros(1, dtype=torch.int32, device=dev)
+    codec.encode_share_vec(blk[2], n, 3, trim=False, out=cpk, offsets=cof)
+    codec.decode_share_vec(packed, offs, n, out=cvec, xs=cxs, bad=cbad)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        codec.encode_share_vec(blk[2], n, 3, trim=False, out=cpk, offsets=cof)
+    e.record()
+    torch.cuda.synchronize()
+    enc_call_ms = s.elapsed_time(e) / reps
+    s.record()
+    for _ in range(reps):
+        codec.decode_share_vec(packed, offs, n, out=cvec, xs=cxs, bad=cbad)
+    e.record()
+    torch.cuda.synchronize()
     dec_call_ms = s.elapsed_time(e) / reps
+    codec.check_bad(cbad)
+    buffers_equal = bool(torch.equal(cvec, blk[2])) and bool(torch.equal(cpk[:total], packed[:total]))
+    del cpk, cof, cvec, cxs
     # the kernels: the C entry points on preallocated buffers, events on their stream
     import ctypes as _ct
 
@@ -683,8 +750,14 @@ def rows_bench(dev, log2n: int) -> dict:
     rows["share_codec"] = {"workload": f"share x=3 of 2^{log2n} elements <-> packed _share_to_bytes records",
                            "encode_ms": enc_ms, "decode_ms": dec_ms, "bytes_out": total,
                            "encode_call_ms": enc_call_ms, "decode_call_ms": dec_call_ms,
+                           "encode_call_alloc_ms": enc_alloc_ms, "decode_call_alloc_ms": dec_alloc_ms,
+                           "decode_call_over_kernel": dec_call_ms / dec_ms,
+                           "api_buffers_equal": buffers_equal,
                            "timing": "encode_ms / decode_ms: the C entry points on preallocated buffers (kernels); "
-                                     "*_call_ms: the Python API calls, allocating their outputs",
+                                     "*_call_ms: the Python API calls on caller buffers (out=, offsets=, xs=; the "
+                                     "decoder's bad-record check deferred: bad=flag, one check after the loop); "
+                                     "*_call_alloc_ms: the API calls allocating their outputs, the decoder "
+                                     "checking per call (a read-back each)",
                            "kernels_equal_api": kernels_equal,
                            "encode_elems_per_s": n / (enc_ms * 1e-3), "decode_elems_per_s": n / (dec_ms * 1e-3),
                            "roundtrip_equal": bool(torch.equal(vec, blk[2])),
@@ -886,6 +959,26 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
         fused_by_buf.append(min(fused))
     fm, um = float(np.median(fused_by_buf)), min(unfused)
     del outs
+    # back to back in a loop, as a caller splitting vector after vector does:
+    # the product default (out=None: each call's block from memory.share_block,
+    # the previous one back to the pool) and a caller's own torch.empty block
+    loop = {}
+    for name in ("pooled_default_out", "caller_out"):
+        ss = shamir.SecretShare(3)
+        ss.random.seed(91)
+        mine = torch.empty((5, field.vec_bytes(n)), dtype=torch.uint8, device=dev) if name == "caller_out" else None
+        for _ in range(3):
+            r = ss.make_shares_vec(sec, 5, out=mine)
+            del r
+        torch.cuda.synchronize()
+        reps_l = 10
+        t0 = time.perf_counter()
+        for _ in range(reps_l):
+            r = ss.make_shares_vec(sec, 5, out=mine)
+            del r
+        torch.cuda.synchronize()
+        loop[name] = (time.perf_counter() - t0) / reps_l * 1e3
+        del mine
     words = 17 * 2 * n
     # smaller vectors take shorter MT substreams (2^10 / 2^12 / 2^14 draws: dn_mt19937_split_device)
     by_size = {}
@@ -915,7 +1008,8 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
             "fused_ms_by_buffer": [x * 1e3 for x in fused_by_buf],
             "timing": "wall time per call; fused_ms: the median over three output buffers of the best of "
                       f"{reps} calls on each (after >= 0.15 s of warm-up calls)",
-            "equal_draw_then_split_and_state": ok, "fused_ms_by_size": by_size}
+            "equal_draw_then_split_and_state": ok, "fused_ms_by_size": by_size,
+            "loop_ms_per_call": loop}
 
 
 def reference_digest_equal(block, n: int, name: str) -> bool:
@@ -955,11 +1049,15 @@ def cold_row(log2n: int) -> dict:
     py = sys.executable
     e2e = _child_json([py, "scripts/cold_call.py", "--log2n", str(log2n), "--mode", "e2e"], 300)
     phases = _child_json([py, "scripts/cold_call.py", "--log2n", str(log2n), "--mode", "phases"], 300)
+    # every probe try misses the keep bar (a fresh process told the fastest rate
+    # is unreachable): the share block's tries run until PROBE_TIME_BUDGET
+    worst = _child_json([py, "scripts/cold_call.py", "--log2n", str(log2n), "--mode", "e2e", "--force-miss"], 300)
     c5 = _child_json([py, "scripts/e2e_round.py", "--cold", "--rounds", "1", "--coeffs", "mt",
                       "--log2n", str(log2n), "--port", str(free_port())], 600)
     return {"workload": f"first make_shares_vec(2^{log2n} int64, 5) of a fresh process, secrets already on "
                         "the device; wall time to return",
             "cold_ms": e2e.get("first_ms"), "warm_after_ms": e2e.get("second_ms"), "first_call": e2e,
+            "cold_worst_ms": worst.get("first_ms"), "cold_worst": worst,
             "phases": phases,
             "config5_first_round": {k: c5.get(k) for k in ("wall_s", "input_MBps", "pack_s", "h2d_s", "split_s",
                                                            "encode_d2h_s", "post_tail_s", "peer_verified", "error")
@@ -1000,6 +1098,24 @@ def byte_api_row(budget_s: float = 2.0) -> dict:
             "cpu_reference_make_shares_us": per_call(lambda: ref.make_shares(secret, n), budget_s / 8),
             "cpu_reference_resolve_shares_us": per_call(lambda: ref.resolve_shares(rsh[:t]), budget_s / 8),
             "roundtrip_ok": bool(ok)}
+    # the share envelope of the same call sites (runner/horizontal/agg.py:192-196
+    # encrypt per share per peer, :258 / :265 decrypt): the byte API on the host
+    # (csrc/host_aes.cpp) beside the device route it replaced (H2D, one launch, D2H)
+    from delta_node.crypto import aes
+    from delta_node.crypto.aes import aes as aes_mod
+
+    key = _os.urandom(32)
+    ae = {"unit": "us per call", "host_cipher": aes.host_impl(), "host_max_bytes": aes.HOST_MAX_BYTES}
+    for nb in (68, 33):
+        data = _os.urandom(nb)
+        text = aes.encrypt(key, data)
+        dev_text = lambda: bytes(aes.encrypt_vec(key, aes_mod._to_device(data)).cpu().numpy())  # noqa: E731
+        ok = aes.decrypt(key, text) == data and aes.decrypt(key, dev_text()) == data
+        ae[f"{nb}B"] = {"encrypt_us": per_call(lambda: aes.encrypt(key, data), budget_s / 8),
+                        "decrypt_us": per_call(lambda: aes.decrypt(key, text), budget_s / 8),
+                        "device_route_encrypt_us": per_call(dev_text, budget_s / 8),
+                        "roundtrip_ok": bool(ok)}
+    out["aes"] = ae
     return out
 
 
@@ -1165,11 +1281,11 @@ def main():
     stream = torch.cuda.current_stream()
 
     # HIP events on the launch stream bracket every kernel of the timed steps:
-    # two per step (before the split, between split and reconstruct); the
-    # reconstruct of step i ends at step i + 1's first event (the last one at
-    # one more).  Each event record is a queue packet of its own, so no third
-    # per step; they are TimingEvents (no system-scope fence per record:
-    # torch's events cost ~4-5 us of stream time each at 2^21, r05g).
+    # three per step (before the split, between split and reconstruct, after
+    # the reconstruct), so each kernel's time excludes the host's launch gap
+    # before the next step (reported apart as step_gap_ms).  They
+    # are TimingEvents (no system-scope fence per record: torch's events cost
+    # ~4-5 us of stream time each at 2^21, r05g).
     def step(i, ev=None):
         b = i % nbuf
         if ev:
@@ -1178,13 +1294,15 @@ def main():
         if ev:
             ev[1].record(stream)
         _native.reconstruct(row_sets[b], w, out_u64=rec, n=N)
+        if ev:
+            ev[2].record(stream)
 
     def timed_steps(fn, steps):
         for i in range(args.warmup):
             fn(i)
         barrier()
         mk = TimingEvent if args.events == "nofence" else (lambda: torch.cuda.Event(enable_timing=True))
-        evs = [[mk() for _ in range(2)] for _ in range(steps)]
+        evs = [[mk() for _ in range(3)] for _ in range(steps)]
         end = mk()
         barrier()
         t0 = time.perf_counter()
@@ -1202,7 +1320,10 @@ def main():
     elapsed, evs = timed_steps(step, args.steps)
     split_each = [evs[i][0].elapsed_time(evs[i][1]) for i in range(args.steps)]
     split_ms = float(np.mean(split_each))
-    recon_ms = float(np.mean([evs[i][1].elapsed_time(evs[i + 1][0]) for i in range(args.steps)]))
+    recon_ms = float(np.mean([evs[i][1].elapsed_time(evs[i][2]) for i in range(args.steps)]))
+    # stream time between one step's reconstruct and the next step's split (host launch gaps)
+    gap_ms = float(np.mean([evs[i][2].elapsed_time(evs[i + 1][0]) for i in range(args.steps - 1)])) \
+        if args.steps > 1 else None
     split_by_buf = [float(np.mean(split_each[b::nbuf])) for b in range(min(nbuf, args.steps))]
 
     # ---- parity of what was timed (cheap, size-independent + sampled) -----
@@ -1250,6 +1371,9 @@ def main():
         ceiling = {"ms": float(np.mean([c["ms"] for c in ceils])), "grid": [c["grid"] for c in ceils],
                    "kernel": ceils[0]["kernel"], "buffers": len(ceils)}
         recon_ceiling = measure_recon_ceiling(share_rows, rec, N)
+        if world == 1:
+            placement["caller_blocks"] = caller_blocks_row(sec, coeffs, N, t, n, nbuf, stream, split_bytes,
+                                                           shares)
     del share_bufs, row_sets
 
     # ---- N > 1: the weak-scaling figure (2^log2n elements per GPU) --------
@@ -1333,10 +1457,15 @@ def main():
                      "events": ("HIP events with hipEventDisableSystemFence on the launch stream"
                                 if args.events == "nofence" else "torch.cuda.Event (system-scope fence per record)"),
                      "placement": placement,
+                     # blocks memory.share_block mapped, probed and rejected for this run's share
+                     # blocks (the probe-and-discard cost of the fractions above)
+                     "probe_rejected_blocks": placement and placement["pool"]["rejected"],
+                     "caller_blocks_frac_mean_time": placement and placement.get("caller_blocks", {}).get(
+                         "frac_mean_time"),
                      "ceiling_measured": ceiling and {
                          **ceiling, "GBps": split_bytes / (ceiling["ms"] * 1e-3) / 1e9,
                          "split_frac_of_ceiling": ceiling["ms"] / split_ms}},
-        "kernels": {"split_ms": split_ms, "reconstruct_ms": recon_ms,
+        "kernels": {"split_ms": split_ms, "reconstruct_ms": recon_ms, "step_gap_ms": gap_ms,
                     "split_GBps": achieved, "reconstruct_GBps": recon_bytes / (recon_ms * 1e-3) / 1e9,
                     "split_elems_per_s": N / (split_ms * 1e-3), "reconstruct_elems_per_s": N / (recon_ms * 1e-3),
                     "reconstruct_ceiling_measured": recon_ceiling and {

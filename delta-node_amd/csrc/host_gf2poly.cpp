@@ -15,10 +15,13 @@
 // make_shares_vec, so the build computes all kMtRtRows
 // once (csrc/gen_mt_rt_rows.cpp -> lib/mt_rt_rows14.bin) and embeds them in
 // the library (csrc/mt_rt_rows14.S, .incbin); at first use the embedded rows
-// are checked — D_1..D_64 against the tabulated rows, and 16 rows spread over
-// the table against the recurrence D_s = D_{s-1} x^L — and used as they are.
-// A library built without the blob, or a blob that fails the check, falls
-// back to computing rows at run time.
+// are checked — the generator's 128-bit checksum of the whole table (two
+// trailing words: a blob damaged after generation), D_1..D_64 against the
+// tabulated rows, and 16 rows spread over the table against the recurrence
+// D_s = D_{s-1} x^L (a wrong computation) — and used as they are.  A library
+// built without the blob (the build host had no carry-less multiply: the
+// Makefile embeds an empty one), or a blob that fails the check, falls back to
+// computing rows at run time.
 #include <immintrin.h>
 
 #include <cstdint>
@@ -147,9 +150,12 @@ extern "C" const uint64_t dn_mt_rt_rows14_blob_end[] __attribute__((weak, visibi
 const uint64_t* embedded_rows() {
   static const uint64_t* checked = [] () -> const uint64_t* {
     const uint64_t* b = dn_mt_rt_rows14_blob;
-    if (!b || !dn_mt_rt_rows14_blob_end ||
-        static_cast<uint64_t>(dn_mt_rt_rows14_blob_end - b) != kMtRtRows * static_cast<uint64_t>(kW))
+    const uint64_t nw = kMtRtRows * static_cast<uint64_t>(kW);
+    if (!b || !dn_mt_rt_rows14_blob_end || static_cast<uint64_t>(dn_mt_rt_rows14_blob_end - b) != nw + 2)
       return nullptr;
+    uint64_t h[2];
+    mt_rt_rows_checksum(b, nw, h);
+    if (h[0] != b[nw] || h[1] != b[nw + 1]) return nullptr;
     for (int s = 1; s <= kMtDirectRows; ++s)
       if (std::memcmp(b + (s - 1) * kW, kDirect14[s - 1], sizeof(uint64_t) * kW)) return nullptr;
     Barrett br;
@@ -164,6 +170,19 @@ const uint64_t* embedded_rows() {
 }
 
 }  // namespace
+
+void mt_rt_rows_checksum(const uint64_t* w, uint64_t n, uint64_t out[2]) {
+  // two independent multiply-rotate chains over the words (not a MAC: it
+  // catches a blob damaged between the generator and the library)
+  uint64_t a = 0x9E3779B97F4A7C15ull ^ n, c = 0xC2B2AE3D27D4EB4Full;
+  for (uint64_t i = 0; i < n; ++i) {
+    a = ((a ^ w[i]) * 0xFF51AFD7ED558CCDull);
+    a ^= a >> 29;
+    c = ((c + w[i]) * 0xC4CEB9FE1A85EC53ull) ^ (c >> 31) ^ i;
+  }
+  out[0] = a;
+  out[1] = c;
+}
 
 bool mt_rt_rows_compute(uint64_t* out, uint64_t nrows) {
   if (!__builtin_cpu_supports("pclmul") || nrows == 0) return false;
@@ -209,3 +228,5 @@ const uint64_t* mt_direct_rows_l14(uint64_t S, uint64_t* version) {
 }
 
 }  // namespace dn
+
+extern "C" int dn_mt19937_rt_rows_embedded(void) { return dn::embedded_rows() ? 1 : 0; }

@@ -76,7 +76,10 @@ extern "C" int dn_i64_sum(const int64_t* const* inputs, int k, int64_t* out, uin
   a.out = out;
   a.n = n;
   a.k = k;
-  const uint64_t blocks = (n / 2 + 255) / 256;
+  // one workgroup per 256 * DN_SUM_WIDE pairs (sized per pair,
+  // 7 of 8 workgroups found no work), at most 8192
+  constexpr uint64_t kPairsPerBlock = 256ull * DN_SUM_WIDE;
+  const uint64_t blocks = (n / 2 + kPairsPerBlock - 1) / kPairsPerBlock;
   // (the member count as a template argument, all loads of a pair issued
   // before the adds: 0.258 ms either way at 10 x 2^24, profiles/r05/m/)
   hipLaunchKernelGGL(i64_sum_kernel, dim3(blocks < 8192 ? (blocks ? blocks : 1) : 8192), dim3(256), 0,

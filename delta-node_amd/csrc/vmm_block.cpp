@@ -9,6 +9,7 @@
 // "caller owns memory" contract is unchanged.  Host code, HIP runtime API only.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -48,6 +49,10 @@ hipError_t on_device(int device, F&& f) {
   if (prev != device && prev >= 0) (void)hipSetDevice(prev);
   return r;
 }
+
+// virtual address space retired by dn_block_free and by failed allocations
+// (their ranges stay reserved; see dn_block_free)
+std::atomic<uint64_t> g_retired{0};
 
 std::mutex& blocks_mutex() {
   static std::mutex* m = new std::mutex;  // never destroyed (the runtime may go first)
@@ -127,6 +132,7 @@ extern "C" int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, 
     // in dn_block_free: no later block is placed where these mappings were)
     for (uint64_t off = 0; off < mapped; off += chunk) (void)hipMemUnmap(static_cast<uint8_t*>(base) + off, chunk);
     for (auto h : b.handles) (void)hipMemRelease(h);
+    g_retired += b.span;
     return set_error(DN_ERR_HIP, "dn_block_alloc: %llu B in %llu-B chunks: %s", static_cast<unsigned long long>(bytes),
                      static_cast<unsigned long long>(chunk), hipGetErrorString(e));
   }
@@ -190,20 +196,22 @@ extern "C" int dn_block_acquire(void* ptr, void* stream, int wait) {
   Block* b = find_block(ptr);
   if (!b) return set_error(DN_ERR_ARG, "dn_block_acquire: not a dn_block_alloc pointer");
   const auto s = static_cast<hipStream_t>(stream);
+  // Two passes: every other-stream use is checked (wait = 0) or waited for
+  // (wait = 1) before any pending flag is cleared, so a RETRY or an error
+  // leaves the block's record exactly as it was — a later free or acquire
+  // still orders after every stream's queued work on it.
   for (auto& u : b->uses) {
-    if (!u.pending) continue;
-    if (u.stream != s) {
-      if (!wait) {
-        const hipError_t q = hipEventQuery(u.event);
-        if (q == hipErrorNotReady) return set_error(DN_ERR_RETRY, "dn_block_acquire: still in use on another stream");
-        if (q != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_acquire: %s", hipGetErrorString(q));
-      } else {
-        const hipError_t e = on_device(b->device, [&] { return hipStreamWaitEvent(s, u.event, 0); });
-        if (e != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_acquire: %s", hipGetErrorString(e));
-      }
+    if (!u.pending || u.stream == s) continue;
+    if (!wait) {
+      const hipError_t q = hipEventQuery(u.event);
+      if (q == hipErrorNotReady) return set_error(DN_ERR_RETRY, "dn_block_acquire: still in use on another stream");
+      if (q != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_acquire: %s", hipGetErrorString(q));
+    } else {
+      const hipError_t e = on_device(b->device, [&] { return hipStreamWaitEvent(s, u.event, 0); });
+      if (e != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_acquire: %s", hipGetErrorString(e));
     }
-    u.pending = false;
   }
+  for (auto& u : b->uses) u.pending = false;  // now ordered before s's next work
   return DN_OK;
 }
 
@@ -215,7 +223,9 @@ extern "C" int dn_block_acquire(void* ptr, void* stream, int wait) {
 // (scripts/msv_block_debug.py, pass r04i: every new block at a freed block's
 // address; never otherwise).  The cost is address space only: 2^47 bytes
 // retire ~25,000 freed 5.5 GB blocks, and frees are rare (the Python pool
-// reuses idle blocks; memory.empty_cache() and pool overflow free).
+// reuses idle blocks; memory.empty_cache() and pool overflow free).  The
+// retired bytes are counted (dn_block_retired_bytes); memory.py stops mapping
+// new blocks — torch.empty instead — once they pass its budget.
 extern "C" int dn_block_free(void* ptr) {
   if (!ptr) return DN_OK;
   Block b;
@@ -247,6 +257,13 @@ extern "C" int dn_block_free(void* ptr) {
   });
   b.uses.clear();
   b.handles.clear();
+  g_retired += b.span;
   if (first != hipSuccess) return set_error(DN_ERR_HIP, "dn_block_free: %s", hipGetErrorString(first));
+  return DN_OK;
+}
+
+extern "C" int dn_block_retired_bytes(uint64_t* bytes) {
+  if (!bytes) return set_error(DN_ERR_ARG, "dn_block_retired_bytes: null pointer");
+  *bytes = g_retired.load();
   return DN_OK;
 }

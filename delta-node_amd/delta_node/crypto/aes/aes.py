@@ -24,7 +24,14 @@ Text that is not canonical base64 / hex (whitespace, missing padding, stray
 '=' or characters outside the alphabet) is parsed on the host with the
 reference's own calls (bytes.fromhex, base64.b64decode), so the result — or
 the exception — is the reference's; the keystream still comes from the GPU
-(dn_aes_ctr).  There is no CPU cipher.
+(dn_aes_ctr).
+
+The byte API (`encrypt` / `decrypt`, one share per call in the reference's
+callers: runner/horizontal/agg.py:192-196, :258, :265) runs on the calling
+core — dn_aes_encrypt_host / dn_aes_decrypt_host (csrc/host_aes.cpp, AES-NI)
+— for messages up to `HOST_MAX_BYTES` and whenever no HIP device is visible: a
+~70-byte share costs ~1 us there against ~100 us of launch and copies.  Larger
+byte messages on a GPU node, and every `*_vec` call, run on the device.
 """
 from __future__ import annotations
 
@@ -36,7 +43,14 @@ from typing import List, Optional, Union
 from ..shamir import _native
 
 EXPORTS = ("dn_aes_expand_key", "dn_aes_ctr", "dn_aes_encrypt_len", "dn_aes_encrypt", "dn_aes_decrypt_capacity",
-           "dn_aes_decrypt")
+           "dn_aes_decrypt", "dn_aes_ctr_host", "dn_aes_encrypt_host", "dn_aes_decrypt_host", "dn_aes_host_impl", "dn_aes_expand_key_host")
+
+# byte-API messages up to this size are sealed / opened on the calling core
+# even on a GPU node (host AES-NI at ~2-4 GB/s beats H2D + launch + D2H below
+# ~1 MiB; the vector API is the device path)
+HOST_MAX_BYTES = 1 << 20
+
+
 def _lib() -> ctypes.CDLL:
     L = _native.lib()
     if not getattr(L, "_dn_aes_bound", False):  # argtypes, once per loaded library
@@ -53,6 +67,16 @@ def _lib() -> ctypes.CDLL:
         L.dn_aes_decrypt_capacity.argtypes = [u64, i32]
         L.dn_aes_decrypt.restype = i32
         L.dn_aes_decrypt.argtypes = [cp, i32, vp, u64, i32, vp, u64, vp, vp, vp]
+        L.dn_aes_ctr_host.restype = i32
+        L.dn_aes_ctr_host.argtypes = [cp, i32, cp, cp, vp, u64]
+        L.dn_aes_encrypt_host.restype = i32
+        L.dn_aes_encrypt_host.argtypes = [cp, i32, cp, cp, u64, vp, i32]
+        L.dn_aes_decrypt_host.restype = i32
+        L.dn_aes_decrypt_host.argtypes = [cp, i32, cp, u64, i32, vp, u64, ctypes.POINTER(ctypes.c_uint64)]
+        L.dn_aes_expand_key_host.restype = i32
+        L.dn_aes_expand_key_host.argtypes = [cp, i32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32)]
+        L.dn_aes_host_impl.restype = i32
+        L.dn_aes_host_impl.argtypes = []
         L._dn_aes_bound = True
     return L
 
@@ -108,9 +132,23 @@ def ctr_vec(key, nonce: bytes, data, out=None):
     return out
 
 
-def encrypt_vec(key, data, *, nonce: Optional[bytes] = None, hex: bool = False):
+_PREFIX = {}  # device index -> the two bytes "0x" on that device
+
+
+def encrypt_buffer(n: int, hex: bool = False, device=None):
+    """A buffer `encrypt_vec(..., out=buf)` can fill for an n-byte message
+    (reused across calls of that size: no allocation per call)."""
+    import torch
+
+    lead = 16 if hex else 0
+    dev = device if device is not None else _native.require_device()
+    return torch.empty(lead + int(_lib().dn_aes_encrypt_len(n, int(hex))), dtype=torch.uint8, device=dev)
+
+
+def encrypt_vec(key, data, *, nonce: Optional[bytes] = None, hex: bool = False, out=None):
     """`aes.encrypt(key, data)` of a device byte vector -> uint8 device tensor of
-    the base64 text, or with hex=True of "0x" + its hex (serialize.bytes_to_hex)."""
+    the base64 text, or with hex=True of "0x" + its hex (serialize.bytes_to_hex).
+    out: a buffer from encrypt_buffer(data.numel(), hex) (the result is a view of it)."""
     import torch
 
     k, iv = _key(key), _nonce(nonce)
@@ -119,14 +157,21 @@ def encrypt_vec(key, data, *, nonce: Optional[bytes] = None, hex: bool = False):
     n = data.numel()
     size = int(L.dn_aes_encrypt_len(n, int(hex)))
     lead = 16 if hex else 0  # the kernel writes from a 16-byte boundary; "0x" goes just in front
-    buf = torch.empty(lead + size, dtype=torch.uint8, device=data.device)
+    if out is None:
+        buf = torch.empty(lead + size, dtype=torch.uint8, device=data.device)
+    else:
+        buf = _u8(out, "encrypt_vec out")
+        if buf.numel() < lead + size or buf.device != data.device or (buf.data_ptr() + lead) % 16:
+            raise ValueError("encrypt_vec: out must come from encrypt_buffer(n, hex) on the data's device")
     _native.check(L.dn_aes_encrypt(k, len(k), iv, _ptr(data), n, buf.data_ptr() + lead, int(hex),
                                    _native.stream_ptr()))
     if not hex:
-        return buf
-    buf[lead - 2] = ord("0")
-    buf[lead - 1] = ord("x")
-    return buf[lead - 2:]
+        return buf[:size]
+    pre = _PREFIX.get(buf.device.index)
+    if pre is None:
+        pre = _PREFIX[buf.device.index] = torch.tensor([ord("0"), ord("x")], dtype=torch.uint8, device=buf.device)
+    buf[lead - 2:lead].copy_(pre)  # one device copy
+    return buf[lead - 2:lead + size]
 
 
 def decrypt_vec(key, text, *, hex: bool = False):
@@ -181,17 +226,70 @@ def _to_device(data: bytes):
     return torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
 
 
+def _bytes(data) -> bytes:
+    """cryptography's update() takes bytes-like data only (a str raises TypeError)."""
+    if isinstance(data, bytes):
+        return data
+    if isinstance(data, (bytearray, memoryview)):
+        return bytes(data)
+    raise TypeError("data must be bytes-like")
+
+
+def ctr_host(key, nonce: bytes, data) -> bytes:
+    """`Cipher(AES(key), CTR(nonce)).encryptor().update(data)` on the calling core."""
+    k, iv, d = _key(key), _nonce(nonce), _bytes(data)
+    out = ctypes.create_string_buffer(len(d))
+    _native.check(_lib().dn_aes_ctr_host(k, len(k), iv, d, out, len(d)))
+    return out.raw
+
+
+def _encrypt_host(k: bytes, iv: bytes, d: bytes) -> bytes:
+    L = _lib()
+    out = ctypes.create_string_buffer(4 * ((len(d) + 18) // 3))
+    _native.check(L.dn_aes_encrypt_host(k, len(k), iv, d, len(d), out, 0))
+    return out.raw
+
+
+def _decrypt_host(k: bytes, text: bytes) -> bytes:
+    L = _lib()
+    cap = int(L.dn_aes_decrypt_capacity(len(text), 0))
+    if cap:
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_uint64()
+        rc = L.dn_aes_decrypt_host(k, len(k), text, len(text), 0, out, cap, ctypes.byref(n))
+        if rc == _native.DN_OK:
+            return out.raw[: n.value]
+        if rc != _native.DN_ERR_RETRY:
+            _native.check(rc)
+    # not canonical base64: the reference's own parse (aes.py:18-19), its errors
+    raw = base64.b64decode(text)
+    return ctr_host(k, raw[:16], raw[16:])
+
+
+def host_impl() -> str:
+    """"aesni" or "table": the host cipher the byte API uses on this CPU."""
+    return "aesni" if _lib().dn_aes_host_impl() else "table"
+
+
 def encrypt(key: bytes, data: bytes, *, nonce: Optional[bytes] = None) -> bytes:
-    """aes.py:8-14: b64encode(nonce + AES-CTR(key, nonce)(data)); nonce = os.urandom(16) by default."""
-    _key(key)
-    if nonce is not None:
-        _nonce(nonce)
-    return bytes(encrypt_vec(key, _to_device(bytes(data)), nonce=nonce).cpu().numpy())
+    """aes.py:8-14: b64encode(nonce + AES-CTR(key, nonce)(data)); nonce = os.urandom(16) by default.
+    On the calling core up to HOST_MAX_BYTES (or without a HIP device), else on the GPU."""
+    k, iv, d = _key(key), _nonce(nonce), _bytes(data)
+    if len(d) <= HOST_MAX_BYTES or not _native.has_device():
+        return _encrypt_host(k, iv, d)
+    return bytes(encrypt_vec(k, _to_device(d), nonce=iv).cpu().numpy())
 
 
 def decrypt(key: bytes, data: Union[bytes, str]) -> bytes:
-    """aes.py:17-23."""
-    _key(key)
+    """aes.py:17-23.  On the calling core up to HOST_MAX_BYTES of text (or
+    without a HIP device), else on the GPU."""
+    k = _key(key)
     if isinstance(data, str):
-        data = data.encode("ascii")
-    return bytes(decrypt_vec(key, _to_device(bytes(data))).cpu().numpy())
+        try:
+            data = data.encode("ascii")
+        except UnicodeEncodeError:
+            raise ValueError("string argument should contain only ASCII characters") from None
+    text = _bytes(data)
+    if len(text) <= HOST_MAX_BYTES or not _native.has_device():
+        return _decrypt_host(k, text)
+    return bytes(decrypt_vec(k, _to_device(text)).cpu().numpy())

@@ -47,7 +47,8 @@ EXPORTS = (
     "dn_mt19937_device_scratch_bytes", "dn_mt19937_draw_coeffs_device", "dn_mt19937_skip",
     "dn_mt19937_split_device", "dn_mt19937_split_supported", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
     "dn_shamir_eval_at_host", "dn_block_granularity", "dn_block_alloc", "dn_block_free", "dn_block_probe_rows",
-    "dn_block_record", "dn_block_ready", "dn_block_acquire",
+    "dn_block_record", "dn_block_ready", "dn_block_acquire", "dn_block_retired_bytes",
+    "dn_mt19937_rt_rows_embedded",
 )
 
 
@@ -166,6 +167,10 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_block_ready.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int)]
     L.dn_block_acquire.restype = i32
     L.dn_block_acquire.argtypes = [vp, vp, i32]
+    L.dn_mt19937_rt_rows_embedded.restype = i32
+    L.dn_mt19937_rt_rows_embedded.argtypes = []
+    L.dn_block_retired_bytes.restype = i32
+    L.dn_block_retired_bytes.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.dn_block_probe_rows.restype = i32
     L.dn_block_probe_rows.argtypes = [vp, ctypes.c_uint32, u64, vp]
     L.dn_mt19937_skip.restype = i32
@@ -215,6 +220,17 @@ def require_device():
             raise RuntimeError("delta_node.crypto.shamir: no HIP device visible; the MI355X path has no CPU fallback")
         _HAS_DEVICE = True
     return torch.device("cuda", torch.cuda.current_device())
+
+
+def has_device() -> bool:
+    """True when a HIP device is visible (cached once seen); never raises."""
+    global _HAS_DEVICE
+    if _HAS_DEVICE:
+        return True
+    import torch
+
+    _HAS_DEVICE = bool(torch.cuda.is_available())
+    return _HAS_DEVICE
 
 
 def stream_ptr() -> int:

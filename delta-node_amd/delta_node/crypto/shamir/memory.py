@@ -45,7 +45,16 @@ most `PROBE_BUDGET` bytes of them, within the device's free memory) are
 mapped and the fastest is kept (the others are freed after the choice, so a
 retry cannot get their pages back).  The first block of a class on a device
 is the fastest of `PROBE_FIRST` (`PROBE_FIRST_SMALL` under 1 GiB) tries, or
-the first to reach `PROBE_FAST`.
+the first to reach `PROBE_FAST`.  A request stops trying once its tries have
+taken `PROBE_TIME_BUDGET` seconds (the best block so far is kept).
+
+A freed block's virtual range stays reserved (csrc/vmm_block.cpp,
+dn_block_free: a range reused at a freed block's address does not give the
+GPU the new mapping).  The retired bytes are counted
+(dn_block_retired_bytes); once they would pass `RETIRE_BUDGET`, share blocks
+are torch.empty memory (the caching allocator reuses its own ranges) and no
+new block is probed, so a long-running process never exhausts the address
+space.
 """
 from __future__ import annotations
 
@@ -53,13 +62,14 @@ import ctypes
 import itertools
 import math
 import threading
+import time
 import weakref
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 from . import _native
 
 __all__ = ["share_block", "chunked_block", "empty_cache", "granularity", "pool_stats", "block_rate",
-           "record_stream"]
+           "record_stream", "retired_bytes"]
 
 CHUNK_BYTES = 16 << 20         # physical chunk of a pooled block
 CHUNKED_MIN_BYTES = 64 << 20   # smaller share blocks: torch.empty
@@ -89,13 +99,20 @@ PROBE_FIRST_SMALL = 4
 PROBE_FAST = 6.8e12            # the first block of a class keeps at once at this tiled-probe rate (B/s)
 PROBE_BUDGET = 48 << 30        # most bytes mapped at once for one request's tries (and
                                # never more than the device has free beyond POOL_MIN_FREE)
+# most wall time one request spends on tries after its first (mapping a 5.5 GB
+# block of 16 MiB chunks ~7.5 ms, its probe ~3 ms; freeing rejected ones): the
+# worst case, every try slow, stays ~50-60 ms instead of PROBE_TRIES tries
+PROBE_TIME_BUDGET = 0.05
+# virtual address space that freed blocks may retire before new share blocks
+# come from torch.empty instead (x86-64 user space: 2^47 bytes)
+RETIRE_BUDGET = 64 << 40
 
 _lock = threading.RLock()
 _idle: Dict[Tuple[int, int, int], List[Tuple[int, int]]] = {}  # (device, nbytes, chunk) -> [(age, ptr)]
 _idle_bytes = 0
 _age = itertools.count()
 _stats = {"allocs": 0, "reuses": 0, "frees": 0, "probed": 0, "rejected": 0, "waits": 0, "busy_skips": 0,
-          "trimmed": 0}
+          "trimmed": 0, "record_failures": 0, "free_failures": 0, "budget_stops": 0, "va_fallbacks": 0}
 _best_rate: Dict[Tuple[int, int, int], float] = {}  # (device, rows, log2 bytes) -> fastest probed write rate (B/s)
 _rates: Dict[int, float] = {}      # block pointer -> its probed write rate
 _live: Dict[int, "weakref.ref"] = {}  # block pointer -> its live _Block (record_stream)
@@ -115,8 +132,22 @@ def _free_ptr(ptr: int, streams: Sequence[int] = ()) -> None:
     L = _native.lib()
     for s in streams:
         _native.check(L.dn_block_record(ptr, s or None))
-    _native.lib().dn_block_free(ptr)
+    if L.dn_block_free(ptr):
+        _stats["free_failures"] += 1
     _stats["frees"] += 1
+
+
+def retired_bytes() -> int:
+    """Virtual address space retired by freed blocks (dn_block_retired_bytes)."""
+    b = ctypes.c_uint64()
+    _native.check(_native.lib().dn_block_retired_bytes(ctypes.byref(b)))
+    return b.value
+
+
+def _sync_device(index: int) -> None:
+    import torch
+
+    torch.cuda.synchronize(index)
 
 
 def _mem_info(index: int) -> Tuple[int, int]:
@@ -146,8 +177,18 @@ class _Block:
         try:
             _live.pop(ptr, None)
             L = _native.lib()
-            for s in self.streams:
-                _native.check(L.dn_block_record(ptr, s or None))
+            try:
+                for s in self.streams:
+                    _native.check(L.dn_block_record(ptr, s or None))
+            except Exception:
+                # an event could not be recorded (a stream destroyed before the
+                # tensor, a HIP error): the block's uses are not all tracked, so
+                # it is neither pooled nor freed on events — the block's device
+                # drains, then the block is freed (and counted)
+                _stats["record_failures"] += 1
+                _sync_device(self.key[0])
+                _free_ptr(ptr)
+                return
             if self.pooled:
                 nbytes = self.key[1]
                 with _lock:
@@ -294,6 +335,9 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
     first = PROBE_FIRST if nbytes >= (1 << 30) else PROBE_FIRST_SMALL
     spare = max(0, _mem_info(dev.index)[0] - POOL_MIN_FREE)  # torch keeps its margin
     tries = max(1, min(most, PROBE_BUDGET // max(1, nbytes), spare // max(1, nbytes)))
+    # every rejected try retires its range: stay within the address-space budget
+    tries = max(1, min(tries, (RETIRE_BUDGET - _retired()) // max(1, nbytes)))
+    t0 = time.perf_counter()
     for k in range(tries):
         try:
             ptr = _alloc_raw(nbytes, chunk_bytes, dev.index)
@@ -311,6 +355,9 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
                 break
         elif rate >= PROBE_KEEP * best:
             break
+        if k + 1 < tries and time.perf_counter() - t0 > PROBE_TIME_BUDGET:
+            _stats["budget_stops"] += 1  # out of time for this request: keep the best so far
+            break
     rate, keep = max(cands)
     stream = _current_stream(dev.index)  # the probe wrote the rejected blocks on this stream
     for r, p in cands:
@@ -320,6 +367,10 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
     _best_rate[kind] = max([best or 0.0] + [r for r, _ in cands])
     _rates[keep] = rate
     return keep
+
+
+def _retired() -> int:
+    return retired_bytes()
 
 
 def block_rate(t) -> Optional[float]:
@@ -405,9 +456,18 @@ def share_block(shape: Union[int, Sequence[int]], device=None):
 
     dev = _device_index(device)
     shape = (int(shape),) if isinstance(shape, int) else tuple(int(s) for s in shape)
-    if math.prod(shape) < CHUNKED_MIN_BYTES:
+    nbytes = math.prod(shape)
+    if nbytes < CHUNKED_MIN_BYTES:
+        return torch.empty(shape, dtype=torch.uint8, device=dev)
+    if _retired() + nbytes > RETIRE_BUDGET and not _has_idle((dev.index, nbytes, CHUNK_BYTES)):
+        _stats["va_fallbacks"] += 1  # address space retired past the budget: no new mappings
         return torch.empty(shape, dtype=torch.uint8, device=dev)
     return chunked_block(shape, CHUNK_BYTES, dev, probe=True)
+
+
+def _has_idle(key) -> bool:
+    with _lock:
+        return bool(_idle.get(key))
 
 
 def empty_cache() -> None:
@@ -424,4 +484,9 @@ def empty_cache() -> None:
 
 def pool_stats() -> dict:
     with _lock:
-        return {**_stats, "idle_blocks": sum(len(v) for v in _idle.values()), "idle_bytes": _idle_bytes}
+        stats = {**_stats, "idle_blocks": sum(len(v) for v in _idle.values()), "idle_bytes": _idle_bytes}
+    try:
+        stats["retired_bytes"] = retired_bytes()
+    except Exception:  # a scripted library without the counter
+        stats["retired_bytes"] = None
+    return stats

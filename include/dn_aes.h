@@ -66,6 +66,35 @@ uint64_t dn_aes_decrypt_capacity(uint64_t n_text, int hex);
 int dn_aes_decrypt(const uint8_t* key, int key_bytes, const void* text, uint64_t n_text, int hex, void* out,
                    uint64_t capacity, uint64_t* out_len, uint32_t* bad, void* stream);
 
+/* ---- host (the byte API: aes.encrypt / aes.decrypt of one share) ----------
+ * The reference seals each ~70-byte share with its own call
+ * (runner/horizontal/agg.py:192-196, decrypt at :258 / :265); these run on the
+ * calling core (AES-NI when the CPU has it, else T-tables) with the same
+ * schedule, counter convention and text as the device entry points above.
+ * All pointers are HOST pointers. */
+
+/* dn_aes_ctr on the host: out[i] = in[i] ^ keystream[i] (aes.py:10-12). */
+int dn_aes_ctr_host(const uint8_t* key, int key_bytes, const uint8_t* iv, const void* in, void* out, uint64_t n);
+
+/* dn_aes_encrypt on the host (aes.py:8-14 with the given nonce): out holds
+ * dn_aes_encrypt_len(n, hex) bytes. */
+int dn_aes_encrypt_host(const uint8_t* key, int key_bytes, const uint8_t* nonce, const void* in, uint64_t n,
+                        void* out, int hex);
+
+/* dn_aes_decrypt on the host (aes.py:17-23) of canonical base64 (hex != 0: of
+ * its hex digits, without "0x"): *out_len = plaintext bytes.  DN_ERR_RETRY
+ * when the text is not canonical (the caller parses it with the reference's
+ * own calls and uses dn_aes_ctr_host). */
+int dn_aes_decrypt_host(const uint8_t* key, int key_bytes, const void* text, uint64_t n_text, int hex, void* out,
+                        uint64_t capacity, uint64_t* out_len);
+
+/* dn_aes_expand_key with a tabulated S-box (the byte API expands the peer's
+ * key on every call): the same words. */
+int dn_aes_expand_key_host(const uint8_t* key, int key_bytes, uint32_t* rk, int32_t* rounds);
+
+/* 1 when the host cipher uses AES-NI, 0 for the table cipher. */
+int dn_aes_host_impl(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -282,8 +282,11 @@ int dn_shamir_eval_at_host(const uint8_t* coeffs_be, const uint64_t* coeff_offse
  *   dn_block_ready    *ready = 1 when every recorded event is on `stream` or
  *                     has completed (the block may be used on `stream` now)
  *   dn_block_acquire  hand the block to work on `stream`: wait = 0 fails with
- *                     DN_ERR_RETRY while another stream's event is pending;
- *                     wait = 1 makes `stream` wait for those events (no host wait)
+ *                     DN_ERR_RETRY while another stream's event is pending
+ *                     (and then changes nothing); wait = 1 makes `stream` wait
+ *                     for those events (no host wait)
+ *   dn_block_retired_bytes  virtual address space retired so far by frees and
+ *                     failed allocations (the caller's budget for new blocks)
  */
 int dn_block_granularity(int device, uint64_t* bytes);
 int dn_block_alloc(uint64_t bytes, uint64_t chunk_bytes, int device, void** ptr);
@@ -291,6 +294,7 @@ int dn_block_free(void* ptr);
 int dn_block_record(void* ptr, void* stream);
 int dn_block_ready(void* ptr, void* stream, int* ready);
 int dn_block_acquire(void* ptr, void* stream, int wait);
+int dn_block_retired_bytes(uint64_t* bytes);
 
 /*
  * Device, async on `stream`.  Zero `rows` rows of `row_bytes` (whole
@@ -305,6 +309,14 @@ int dn_block_probe_rows(void* ptr, uint32_t rows, uint64_t row_bytes, void* stre
  * `words` getrandbits(32) calls would) by jump-ahead instead of stepping.
  */
 int dn_mt19937_skip(uint32_t* mt_state, int32_t* mt_index, uint64_t words);
+
+/*
+ * Host, diagnostic.  1 when the library's build-time table of MT19937 jump
+ * rows (the 2^24-draw direct level) is present and passes its checks —
+ * checksum, tabulated rows, recurrence — so a first draw uses it; 0 when the
+ * rows would be computed at run time instead.
+ */
+int dn_mt19937_rt_rows_embedded(void);
 
 /*
  * Share wire codec over whole vectors (shamir.py:28-45 `_share_to_bytes` /

@@ -10,6 +10,9 @@ fresh process (bench.py starts it as a child); prints one JSON line.
                  share-block mapping + probe, the MT jump rows and job tables,
                  their upload, the draw + split.  Then the same call again
                  after the first output is dropped (the pool's idle block).
+  --force-miss   every share-block probe try misses the keep bar (the
+                 class's best rate set unreachable, PROBE_FAST likewise): the
+                 worst first call, tries bounded by memory.PROBE_TIME_BUDGET.
   --mode phases  the same costs one at a time: the share block alone
                  (memory.share_block: chunk mapping + write-rate probe), a
                  first 2^12 call (kernels, scratch), then the first 2^N call
@@ -30,6 +33,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--log2n", type=int, default=24)
     ap.add_argument("--mode", choices=("e2e", "phases"), default="e2e")
+    ap.add_argument("--force-miss", action="store_true")
     args = ap.parse_args()
     t_start = time.perf_counter()
     import numpy as np
@@ -59,6 +63,10 @@ def main() -> int:
         torch.cuda.synchronize()
         return r, (time.perf_counter() - t0) * 1e3
 
+    if args.force_miss:
+        memory.PROBE_FAST = float("inf")
+        kind = (0, 5, (5 * field.vec_bytes(n)).bit_length())  # the share block's class (memory._alloc_probed)
+        memory._best_rate[kind] = float("inf")
     ss = shamir.SecretShare(3)
     ss.random.seed(9)
     if args.mode == "e2e":

@@ -159,6 +159,43 @@ def test_bytes_api():
     assert aes.encrypt(key, b"abc") != aes.encrypt(key, b"abc")  # os.urandom nonce, as the reference
 
 
+@pytest.mark.parametrize("n", [0, 1, 33, 68, 100, 4099, 70000])
+def test_host_and_device_agree(n, monkeypatch):
+    """The byte API's host cipher (csrc/host_aes.cpp) and the device kernels give
+    the same text at a fixed nonce, and each opens the other's; above
+    HOST_MAX_BYTES the byte API takes the device path (same bytes)."""
+    from delta_node.crypto.aes import aes as aes_mod
+
+    data = rand_bytes(n, 50 + n)
+    for key in KEYS:
+        for nonce in NONCES:
+            text = aes.encrypt(key, data, nonce=nonce)  # host (n <= HOST_MAX_BYTES)
+            assert text == host(aes.encrypt_vec(key, to_dev(data), nonce=nonce))
+            assert host(aes.decrypt_vec(key, to_dev(text))) == data
+            assert aes.decrypt(key, text) == data
+            assert aes.ctr_host(key, nonce, data) == host(aes.ctr_vec(key, nonce, to_dev(data)))
+    monkeypatch.setattr(aes_mod, "HOST_MAX_BYTES", 0)  # every byte message through the GPU
+    text = aes.encrypt(KEYS[0], data, nonce=NONCES[3])
+    assert text == want_text(KEYS[0], NONCES[3], data)
+    assert aes.decrypt(KEYS[0], text) == data
+
+
+def test_encrypt_into_a_reused_buffer():
+    """encrypt_vec(..., out=encrypt_buffer(n, hex)): the same text as the
+    allocating call, written into the caller's buffer."""
+    key = KEYS[0]
+    for n in (0, 1, 47, 4099):
+        data = to_dev(rand_bytes(n, n + 3))
+        for hex_ in (False, True):
+            buf = aes.encrypt_buffer(n, hex_, dev())
+            for nonce in NONCES[:2]:
+                got = aes.encrypt_vec(key, data, nonce=nonce, hex=hex_, out=buf)
+                assert host(got) == want_text(key, nonce, host(data), hex_)
+                assert buf.data_ptr() <= got.data_ptr() < buf.data_ptr() + buf.numel()
+    with pytest.raises(ValueError):
+        aes.encrypt_vec(key, to_dev(b"x" * 100), hex=True, out=aes.encrypt_buffer(10, True, dev()))
+
+
 def test_large_message_sampled_against_oracle():
     n = (1 << 26) + 77
     g = torch.Generator(device=dev())

@@ -86,6 +86,40 @@ def test_decode_reduces_like_resolve_and_flags_oversize():
         codec.decode_share_vec(bad, torch.tensor([0, bad.numel()], dtype=torch.int64, device=dev()), 1)
 
 
+def test_caller_buffers_and_deferred_bad_check():
+    """encode / decode into caller buffers (no allocation),
+    the decoder's bad-record count added to a caller flag without a sync per
+    call and checked once (codec.check_bad) — same bytes as the allocating form."""
+    n = 5000
+    rng = random.Random(7)
+    vals = [rng.randrange(P) >> rng.randrange(0, 521) for _ in range(n)]
+    vec = torch.from_numpy(field.ints_to_vec(vals)).to(dev())
+    want_p, want_o = codec.encode_share_vec(vec, n, 3)
+    out = torch.empty(codec.encoded_capacity(n, 3), dtype=torch.uint8, device=dev())
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev())
+    p2, o2 = codec.encode_share_vec(vec, n, 3, out=out, offsets=offs)
+    assert p2.data_ptr() == out.data_ptr() and torch.equal(p2, want_p) and torch.equal(o2, want_o)
+    dv = torch.empty(field.vec_bytes(n), dtype=torch.uint8, device=dev())
+    dx = torch.empty(n, dtype=torch.int64, device=dev())
+    flag = torch.zeros(1, dtype=torch.int32, device=dev())
+    for _ in range(3):
+        v2, x2 = codec.decode_share_vec(want_p, want_o, n, out=dv, xs=dx, bad=flag)
+    codec.check_bad(flag)
+    assert v2.data_ptr() == dv.data_ptr() and field.vec_to_ints(dv.cpu().numpy(), n) == vals
+    assert torch.all(x2 == 3)
+    bad = torch.tensor(list(share_to_bytes(2, 1 << 560)), dtype=torch.uint8, device=dev())
+    bo = torch.tensor([0, bad.numel()], dtype=torch.int64, device=dev())
+    codec.decode_share_vec(bad, bo, 1, bad=flag)
+    codec.decode_share_vec(bad, bo, 1, bad=flag)
+    assert int(flag.item()) == 2  # added to, not overwritten
+    with pytest.raises(ValueError, match="2 records"):
+        codec.check_bad(flag)
+    with pytest.raises(ValueError):
+        codec.decode_share_vec(want_p, want_o, n, out=dv[:10])
+    with pytest.raises(ValueError):
+        codec.decode_share_vec(want_p, want_o, n, bad=torch.zeros(1, dtype=torch.int64, device=dev()))
+
+
 def test_byte_api_fixture_through_vector_codec():
     """f3 edge cases: each case's shares, re-encoded from one-element vectors, equal the reference bytes."""
     f3 = load_json("f3_edge.json")

@@ -276,6 +276,72 @@ def test_record_stream_orders_reuse_after_a_second_stream():
     memory.empty_cache()
 
 
+def test_retry_acquire_keeps_every_streams_order():
+    """a block used on streams A and B goes idle with both
+    reads queued.  A request on A must not take it while B is busy — and the
+    refused request must leave A's record intact, so that once B is done a
+    request on a third stream C still waits for A (dn_block_acquire checks
+    every stream before it clears any).  Then C's write lands after A's read."""
+    memory.empty_cache()
+    shape = (5, field.vec_bytes(1 << 18))
+    sa, sb, sc = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(sa):
+        x = memory.chunked_block(shape, device=dev())
+        x.fill_(0x3C)
+        key = (dev().index, x.numel(), memory.CHUNK_BYTES)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(sa):
+        _busy(3000)
+        kept_a = x.clone()  # A's read, queued behind 3 s
+    with torch.cuda.stream(sb):
+        _busy(300)
+        kept_b = x.clone()  # B's read, queued behind 0.3 s
+    memory.record_stream(x, sb)
+    del x
+    gc.collect()
+    assert memory._take_idle(key, sa.cuda_stream) is None  # B still busy: RETRY, nothing changed
+    sb.synchronize()
+    a_busy = not sa.query()
+    assert memory._take_idle(key, sc.cuda_stream) is None  # A's read is still pending
+    assert a_busy, "stream A finished before the request on C: the test did not race"
+    ptr = memory._take_idle(key, sc.cuda_stream, wait=True)  # C waits for A on the device
+    assert ptr is not None
+    with torch.cuda.stream(sc):
+        blk = memory._Block(ptr, key, shape, True, sc.cuda_stream)
+        y = torch.as_tensor(blk, device=dev())
+        y.fill_(0xC3)
+    torch.cuda.synchronize()
+    assert int((kept_a != 0x3C).sum().item()) == 0 and int((kept_b != 0x3C).sum().item()) == 0
+    assert int((y != 0xC3).sum().item()) == 0
+    del y, blk, kept_a, kept_b
+    gc.collect()
+    memory.empty_cache()
+
+
+def test_unpooled_allocate_free_loop_counts_retired_space(monkeypatch):
+    """every freed block retires its range; the count is
+    exact, and past RETIRE_BUDGET share_block hands out torch.empty memory
+    instead of mapping (and later retiring) new ranges."""
+    memory.empty_cache()
+    shape = (2, 32 << 20)  # 64 MiB: a chunked share block
+    r0 = memory.retired_bytes()
+    for _ in range(20):
+        x = memory.chunked_block(shape, device=dev(), pooled=False)
+        x.fill_(7)
+        del x
+        gc.collect()
+    torch.cuda.synchronize()
+    assert memory.retired_bytes() - r0 == 20 * (64 << 20)
+    monkeypatch.setattr(memory, "RETIRE_BUDGET", memory.retired_bytes() + (32 << 20))
+    before = memory.pool_stats()["va_fallbacks"]
+    y = memory.share_block(shape, dev())
+    assert memory.pool_stats()["va_fallbacks"] == before + 1 and memory.block_rate(y) is None
+    y.fill_(1)
+    assert int(y.sum().item()) == y.numel()
+    del y
+    memory.empty_cache()
+
+
 def test_make_shares_vec_t4_loop_on_a_side_stream_equals_host_draw():
     """t = 4 takes the draw-then-split path: its coefficient block (pooled,
     >= 64 MiB here) is dropped right after the split is queued, and every

@@ -45,6 +45,16 @@ def test_library_exports_header_symbols():
     assert sorted(_native.EXPORTS + _mask_native.EXPORTS + codec.EXPORTS + mimc7.EXPORTS + aes.EXPORTS) == syms
 
 
+def test_embedded_mt_jump_rows_pass_their_checks():
+    """The build-time table of 2048 direct jump rows (csrc/gen_mt_rt_rows.cpp,
+    embedded by csrc/mt_rt_rows14.S) carries its generator's checksum and
+    passes it, the 64 tabulated rows and the recurrence at first use
+    (csrc/host_gf2poly.cpp): a first 2^24 draw does not recompute it."""
+    assert _native.lib().dn_mt19937_rt_rows_embedded() == 1
+    blob = os.path.join(ROOT, "delta-node_amd", "lib", "mt_rt_rows14.bin")
+    assert os.path.getsize(blob) == 8 * (2048 * 312 + 2)
+
+
 def test_version_and_sizes():
     assert "gfx950" in _native.version()
     for n in (0, 1, 255, 256, 257, 1 << 20, (1 << 24) + 3):

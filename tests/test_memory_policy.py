@@ -43,6 +43,7 @@ def fake(monkeypatch):
         monkeypatch.setattr(memory, "_current_stream", lambda index: 0)
         monkeypatch.setattr(memory, "_mem_info", lambda index: (1 << 50, 1 << 50))
         monkeypatch.setattr(memory, "PROBE_FIRST_SMALL", 2)  # the tests below script two first tries
+        monkeypatch.setattr(memory, "_retired", lambda: 0)
         return f
     return make
 
@@ -155,8 +156,13 @@ class FakeLib:
         self.freed = []
 
     def dn_block_record(self, ptr, stream):
+        if ptr in self.fail_record:
+            return memory._native.DN_ERR_HIP
         self.recorded.append((ptr, stream or 0))
         return 0
+
+    def dn_last_error(self):
+        return b"scripted HIP error"
 
     def dn_block_acquire(self, ptr, stream, wait):
         if ptr in self.busy and not wait:
@@ -167,6 +173,8 @@ class FakeLib:
     def dn_block_free(self, ptr):
         self.freed.append(ptr)
         return 0
+
+    fail_record = ()
 
 
 @pytest.fixture
@@ -179,6 +187,8 @@ def pool(monkeypatch):
     monkeypatch.setattr(memory, "_rates", {})
     monkeypatch.setattr(memory, "_live", {})
     monkeypatch.setattr(memory, "_mem_info", lambda index: (state["free"], 288 << 30))
+    L.synced = []
+    monkeypatch.setattr(memory, "_sync_device", lambda index: L.synced.append(index))
     L.state = state
     return L
 
@@ -274,3 +284,54 @@ def test_first_small_block_is_the_fastest_of_probe_first_small(fake, monkeypatch
     g = fake([5.0, 7.0, 9.0])
     q = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # 1 GiB and up: the faster of PROBE_FIRST = 2
     assert g.rate_of[q] == 7.0 and g.rates == [9.0]
+
+
+def test_failed_record_frees_the_block_after_a_device_wait(pool):
+    """ADVICE/VERDICT r05: a block whose event cannot be recorded is neither
+    pooled nor leaked — its device drains, then it is freed, and counted."""
+    before = memory._stats["record_failures"]
+    pool.fail_record = {0x100}
+    b = memory._Block(0x100, KEY, (KEY[1],), True, 7)
+    del b
+    assert pool.freed == [0x100] and pool.synced == [0]
+    assert KEY not in memory._idle and memory._idle_bytes == 0
+    assert memory._stats["record_failures"] == before + 1
+
+
+def test_time_budget_stops_the_tries(fake, monkeypatch):
+    """Every try slow: the request stops once PROBE_TIME_BUDGET has passed and
+    keeps the best block so far (the cold worst case stays bounded)."""
+    f = fake([7.0, 6.0] + [5.0, 5.1, 5.2, 5.3, 5.4, 5.5, 5.6, 5.7] + [9.9])
+    memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # best 7.0
+    clock = iter([0.0] + [0.02 * k for k in range(1, 100)])  # each try takes 20 ms
+    monkeypatch.setattr(memory.time, "perf_counter", lambda: next(clock))
+    before = memory._stats["budget_stops"]
+    p = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)
+    # tries at 20 / 40 / 60 ms: the third ends past the 50 ms budget
+    assert f.rate_of[p] == 5.2 and f.rates[0] == 5.3 and memory._stats["budget_stops"] == before + 1
+
+
+def test_retire_budget_limits_the_tries(fake, monkeypatch):
+    """Rejected tries retire their ranges: a request never plans more tries
+    than the address-space budget has room for."""
+    f = fake([7.0, 6.0, 5.0, 5.1, 5.2, 9.9])
+    memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # best 7.0
+    monkeypatch.setattr(memory, "_retired", lambda: memory.RETIRE_BUDGET - 2 * NBIG)
+    p = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)
+    assert f.rate_of[p] == 5.1 and f.rates == [5.2, 9.9]  # two tries
+
+
+def test_share_block_past_the_retire_budget_is_torch_memory(monkeypatch):
+    import torch
+
+    calls = []
+    monkeypatch.setattr(memory, "_device_index", lambda device: torch.device("cpu"))
+    monkeypatch.setattr(memory, "chunked_block", lambda *a, **k: calls.append(a) or "chunked")
+    monkeypatch.setattr(memory, "_idle", {})
+    monkeypatch.setattr(memory, "_retired", lambda: 0)
+    assert memory.share_block((2, 64 << 20)) == "chunked"
+    monkeypatch.setattr(memory, "_retired", lambda: memory.RETIRE_BUDGET - (64 << 20))
+    before = memory._stats["va_fallbacks"]
+    t = memory.share_block((2, 64 << 20))
+    assert isinstance(t, torch.Tensor) and t.shape == (2, 64 << 20) and len(calls) == 1
+    assert memory._stats["va_fallbacks"] == before + 1
