@@ -20,6 +20,8 @@
 // per-segment raw offsets.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "dn_internal.hpp"
@@ -54,6 +56,7 @@ struct AccArgs {
   u128 jA[64], jG[64];            // T^(2^k) = (A, G)
   u128 A64;
   uint32_t* rejects;
+  u128 strideA, strideG;  // T^(nwaves * kChunkElems): a wave's step from one tile to its next (small tiles)
 };
 
 __device__ __forceinline__ uint64_t xsl_rr(u128 s) {
@@ -241,6 +244,125 @@ __global__ void __launch_bounds__(kMaskBlock) bounded_acc_kernel(const AccArgs a
 }
 
 
+// DN_MASK_SMALL: tiles of one chunk (512 elements per wave) and no LDS.  A
+// wave's lane g keeps generator g's state at the wave's tile start in
+// registers and steps it to the wave's next tile by one constant map
+// (strideA, strideG: T^(nwaves 512), from the host) instead of a binary
+// jump per tile; each lane offsets it by T^lane per generator.  No generator
+// state crosses a tile, so nothing lives in LDS and occupancy is set by the
+// registers alone (the 4096-element tiles keep 16 B per lane per generator in
+// LDS between chunks: 40 KB per workgroup at 10 generators, 4 waves per SIMD).
+#ifndef DN_MASK_SMALL
+#define DN_MASK_SMALL 0
+#endif
+#ifndef DN_MASK_WAVES
+#define DN_MASK_WAVES 5  // launch bound: waves per SIMD the small-tile kernel is compiled for
+#endif
+
+template <bool MERS, bool NEG, int K>
+__device__ __forceinline__ uint32_t gens_step_small(const AccArgs& a, const u128 sg, const u128 Al, const u128 Gl,
+                                                    const int g, uint64_t (&acc)[kDrawsPerLane]) {
+  u128 st[K], c[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    // generator g + j's tile-start state, from lane g + j, offset by T^lane
+    st[j] = Al * bcast_u128(sg, g + j) + a.inc[g + j] * Gl;
+    c[j] = a.c64[g + j];
+  }
+  return draws_chunk<MERS, NEG, K>(st, acc, a.A64, c, a.excl, a.threshold) << g;
+}
+
+template <bool MERS>
+__global__ void __launch_bounds__(kMaskBlock, DN_MASK_WAVES) bounded_acc_small_kernel(const AccArgs a) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
+  const uint64_t n = a.elem_end - a.elem_begin;
+  const uint64_t ntiles = (n + kChunkElems - 1) / kChunkElems;
+  const uint64_t nwaves = static_cast<uint64_t>(gridDim.x) * (kMaskBlock / 64);
+  const uint64_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (kMaskBlock / 64) + (tid >> 6));
+  if (wave0 >= ntiles) return;
+  uint32_t rejmask = 0u;
+  // T^lane = (Al, Gl), once
+  u128 Al = 1, Gl = 0;
+#pragma unroll 1
+  for (int k = 0; k < 6; ++k) {
+    if ((lane >> k) & 1u) {
+      Gl = a.jA[k] * Gl + a.jG[k];
+      Al = a.jA[k] * Al;
+    }
+  }
+  // lane g: generator g before the wave's first tile (raw draw r uses T^(r+1)), one binary jump
+  u128 sg = 0, cs = 0;
+  if (a.ngen > 0) {
+    uint64_t my_off = 0;
+    u128 my_s0 = 0, my_inc = 0;
+#pragma unroll 1
+    for (int g = 0; g < a.ngen; ++g) {
+      if (lane == static_cast<uint32_t>(g)) {
+        my_off = a.raw_off[g];
+        my_s0 = a.state0[g];
+        my_inc = a.inc[g];
+      }
+    }
+    const uint64_t r = my_off + a.elem_begin + wave0 * kChunkElems + 1;
+    u128 A = 1, G = 0;
+#pragma unroll 1
+    for (int k = 0; k < 64; ++k) {
+      const uint64_t rk = r >> k;
+      if (!__any(rk != 0)) break;
+      if (rk & 1u) {
+        G = a.jA[k] * G + a.jG[k];
+        A = a.jA[k] * A;
+      }
+    }
+    sg = A * my_s0 + my_inc * G;
+    cs = my_inc * a.strideG;  // this lane's generator: the tile-to-tile step's additive term
+  }
+#pragma unroll 1
+  for (uint64_t tile = wave0; tile < ntiles; tile += nwaves) {
+    const uint64_t ec = a.elem_begin + tile * kChunkElems + lane;
+    const bool full = a.elem_begin + (tile + 1) * kChunkElems <= a.elem_end;
+    uint64_t acc[kDrawsPerLane];
+    if (a.base_i64) {
+#pragma unroll
+      for (int i = 0; i < kDrawsPerLane; ++i) {
+        const uint64_t e = ec + 64u * i;
+        acc[i] = (full || e < a.elem_end) ? static_cast<uint64_t>(a.base_i64[e]) : 0u;
+      }
+    } else if (a.base_f64) {
+#pragma unroll
+      for (int i = 0; i < kDrawsPerLane; ++i) {
+        const uint64_t e = ec + 64u * i;
+        acc[i] = (full || e < a.elem_end) ? static_cast<uint64_t>(f64_to_i64_x86(a.base_f64[e] * a.scale)) : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kDrawsPerLane; ++i) acc[i] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kDrawsPerLane; ++i) acc[i] += a.low_total;
+    int g = 0;
+#pragma unroll 1
+    for (; g + 1 < a.npos; g += 2) rejmask |= gens_step_small<MERS, false, 2>(a, sg, Al, Gl, g, acc);
+    if (g < a.npos) rejmask |= gens_step_small<MERS, false, 1>(a, sg, Al, Gl, g++, acc);
+#pragma unroll 1
+    for (; g + 1 < a.ngen; g += 2) rejmask |= gens_step_small<MERS, true, 2>(a, sg, Al, Gl, g, acc);
+    if (g < a.ngen) rejmask |= gens_step_small<MERS, true, 1>(a, sg, Al, Gl, g, acc);
+#pragma unroll
+    for (int i = 0; i < kDrawsPerLane; ++i) {
+      const uint64_t e = ec + 64u * i;
+      if (full || e < a.elem_end) __builtin_nontemporal_store(static_cast<int64_t>(acc[i]), a.out + e);
+    }
+    sg = a.strideA * sg + cs;  // lane g: generator g to the wave's next tile
+  }
+  if (a.rejects) {
+#pragma unroll 1
+    for (int g = 0; g < a.ngen; ++g) {
+      if (__ballot((rejmask >> g) & 1u) && lane == 0) atomicAdd(a.rejects + a.orig[g], 1u);
+    }
+  }
+}
+
 struct RejArgs {
   u128 state0, inc, c64;
   u128 jA[64], jG[64];
@@ -297,6 +419,18 @@ static double pow10_exact(int p) {
   return s;
 }
 
+// T^m = (A, G) from the power-of-two table (host)
+static void pcg64_jump(uint64_t m, const u128* jA, const u128* jG, u128* A, u128* G) {
+  u128 a = 1, g = 0;
+  for (int k = 0; k < 64 && (m >> k); ++k)
+    if ((m >> k) & 1u) {
+      g = jA[k] * g + jG[k];
+      a = jA[k] * a;
+    }
+  *A = a;
+  *G = g;
+}
+
 static int grid_for_tiles(uint64_t tiles) {
   const uint64_t blocks = (tiles + 3) / 4;
   return static_cast<int>(blocks < 8192 ? (blocks ? blocks : 1) : 8192);
@@ -348,13 +482,27 @@ extern "C" int dn_bounded_i64_accumulate(const dn_pcg64_t* gens, const int32_t* 
     }
     if (pass == 0) a.npos = slot;
   }
-  const uint64_t tiles = (elem_end - elem_begin + kTileElems - 1) / kTileElems;
-  const dim3 grid(grid_for_tiles(tiles)), block(kMaskBlock);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.excl == (1ull << kMersK) - 1) a.mers_k = kMersK;  // Lemire by shifts (make_mask's range)
-  const size_t lds = static_cast<size_t>(ngen) * kMaskBlock * sizeof(u128);
-  if (a.mers_k) hipLaunchKernelGGL(bounded_acc_kernel<true>, grid, block, lds, s, a);
-  else hipLaunchKernelGGL(bounded_acc_kernel<false>, grid, block, lds, s, a);
+  const char* sm = tune_env("DN_MASK_SMALL");
+  if (sm ? sm[0] == '1' : DN_MASK_SMALL) {
+    // small tiles: a resident grid (DN_MASK_GRID workgroups per CU), each wave
+    // stepping through its tiles by the constant map T^(nwaves 512)
+    const uint64_t tiles = (elem_end - elem_begin + kChunkElems - 1) / kChunkElems;
+    const char* gc = tune_env("DN_MASK_GRID");
+    const uint64_t per_cu = gc ? static_cast<uint64_t>(std::atoi(gc)) : static_cast<uint64_t>(DN_MASK_WAVES);
+    const uint64_t cap = static_cast<uint64_t>(device_cu_count()) * (per_cu ? per_cu : 1);
+    const uint64_t blocks = std::min<uint64_t>((tiles + 3) / 4, cap);
+    pcg64_jump(4ull * blocks * kChunkElems, a.jA, a.jG, &a.strideA, &a.strideG);
+    if (a.mers_k) hipLaunchKernelGGL(bounded_acc_small_kernel<true>, dim3(blocks), dim3(kMaskBlock), 0, s, a);
+    else hipLaunchKernelGGL(bounded_acc_small_kernel<false>, dim3(blocks), dim3(kMaskBlock), 0, s, a);
+  } else {
+    const uint64_t tiles = (elem_end - elem_begin + kTileElems - 1) / kTileElems;
+    const dim3 grid(grid_for_tiles(tiles)), block(kMaskBlock);
+    const size_t lds = static_cast<size_t>(ngen) * kMaskBlock * sizeof(u128);
+    if (a.mers_k) hipLaunchKernelGGL(bounded_acc_kernel<true>, grid, block, lds, s, a);
+    else hipLaunchKernelGGL(bounded_acc_kernel<false>, grid, block, lds, s, a);
+  }
   const hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(DN_ERR_HIP, "dn_bounded_i64_accumulate: %s", hipGetErrorString(err));
   return DN_OK;

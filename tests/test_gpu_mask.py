@@ -128,3 +128,27 @@ def test_raw_offsets_and_ranges():
     o = out.cpu().numpy()
     assert np.array_equal(o[1234:8000], ref[1234 + 37:8000 + 37])
     assert not o[:1234].any() and not o[8000:].any()
+
+
+@pytest.mark.parametrize("grid", [None, "1"])
+def test_small_tile_kernel_matches(grid, monkeypatch):
+    """The small-tile accumulate (DN_MASK_SMALL, csrc/mask_pcg64.hip: 512-element
+    tiles, generator states in registers stepped tile to tile by T^(nwaves 512))
+    through the tuning build: the reference's fixture and 2^24 digests, signed
+    sums of 12 / 16 / 19 generators, the exact replay on rejections and the
+    segment API — with the default resident grid and with one workgroup per CU
+    (every wave stepping through many tiles)."""
+    from delta_node.crypto.shamir import _native
+
+    monkeypatch.setenv("DN_MASK_SMALL", "1")
+    if grid:
+        monkeypatch.setenv("DN_MASK_GRID", grid)
+    with _native.library(_native.TUNING_LIB):
+        test_make_mask_matches_reference_fixture()
+        test_make_mask_digests_up_to_2e24()
+        for n in (1, 511, 513, 70001):
+            test_make_mask_ragged_vs_numpy(n)
+        for k in (12, 16, 19):
+            test_masked_sum_matches_reference_composition(k)
+        test_exact_replay_on_rejections()
+        test_raw_offsets_and_ranges()
