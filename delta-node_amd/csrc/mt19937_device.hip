@@ -1732,12 +1732,16 @@ void launch_gen(GenArgs& ga, hipStream_t s) {
     // DN_MT_PC_FORCE (tuning build): 0 = the one-wave kernel (A/B)
     const char* pf = tune_env("DN_MT_PC_FORCE");
     const bool pc = !(pf && pf[0] == '0');
+    // DN_MT_GEN_SUBS (tuning build, timing probe only: the output is partial and
+    // CPython's final state is not computed): launch only the first K substream
+    // workgroups — how the generation's time scales with the substreams in flight
+    uint32_t grid = ga.S + 1;
+    if (const char* gs = tune_env("DN_MT_GEN_SUBS")) grid = std::min<uint32_t>(grid, std::max(1, std::atoi(gs)));
     if (pc) {
       if (T == 3 && ga.n_shares == 5)
-        hipLaunchKernelGGL((mt_gen_pc_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(128), lds_words * 4u, s,
-                           ga);
+        hipLaunchKernelGGL((mt_gen_pc_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(grid), dim3(128), lds_words * 4u, s, ga);
       else
-        hipLaunchKernelGGL((mt_gen_pc_kernel<T>), dim3(ga.S + 1), dim3(128), lds_words * 4u, s, ga);
+        hipLaunchKernelGGL((mt_gen_pc_kernel<T>), dim3(grid), dim3(128), lds_words * 4u, s, ga);
       return;
     }
   }
