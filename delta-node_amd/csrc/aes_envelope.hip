@@ -69,12 +69,6 @@
 #ifndef DN_AES_DEC_SPLIT
 #define DN_AES_DEC_SPLIT 2
 #endif
-// DN_AES_DEC_NB: keystream blocks of a decrypt_fused_kernel unit whose rounds
-// run interleaved (3) or one block at a time (1, default: fewer registers with
-// the next unit's text held; 1.67-1.70 vs 1.76-1.81 ms)
-#ifndef DN_AES_DEC_NB
-#define DN_AES_DEC_NB 1
-#endif
 // DN_AES_DEC_COAL (default 1): decode_kernel reads a wave's hex text line by
 // line and transposes it (as the encrypt kernel's text stores); 2 reads half
 // lines (hex_coalesce_half): slower, 1.98-2.01 vs 1.94-1.96 ms
@@ -1054,13 +1048,19 @@ __device__ void decode_unit_slow(const uint8_t* dec, const AesArgs& a, uint64_t 
 // (hex_coalesce: load v of lane l is chunk l >> 3 of lane 8 v + (l & 7); base64:
 // b64_coalesce), the chunk after a unit (skew) from the next lane (the next
 // wave's first chunk for lane 63); otherwise each lane its own unit.
-template <bool HEX>
-__device__ __forceinline__ void load_unit_text(const AesArgs& a, uint64_t gq, uint32_t lane,
-                                             uint32_t (&R)[HEX ? 36 : 20]) {
+// Split in two (round 6): issue_unit_text issues the loads and returns the
+// mode (1: coalesced, wave-uniform), finish_unit_text transposes once they have
+// arrived — so a loop can keep the next unit's loads in flight across this
+// unit's AES.  (With the transpose inside the load, the loads were waited for
+// at once: every unit's text latency was exposed.)
+// WHOLE: the caller guarantees all 64 lanes are active (no ballot, always coalesced)
+template <bool HEX, bool WHOLE = false>
+__device__ __forceinline__ uint32_t issue_unit_text(const AesArgs& a, uint64_t gq, uint32_t lane,
+                                                    uint32_t (&R)[HEX ? 36 : 20]) {
   constexpr int NV = HEX ? 8 : 4;      // 16-B vectors of one unit's text
   const uint64_t tb = HEX ? 128 : 64;  // text bytes per unit
   if constexpr (!HEX && DN_AES_DEC_COAL) {
-    if (__ballot(1) == ~0ull) {  // base64 text: 4 chunks per lane, as the encrypt stores
+    if (WHOLE || __ballot(1) == ~0ull) {  // base64 text: 4 chunks per lane, as the encrypt stores
       const uint64_t w0 = tb * (gq - lane);
       const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 64 * (lane & 15u) + 16 * (lane >> 4));
 #pragma unroll
@@ -1068,24 +1068,15 @@ __device__ __forceinline__ void load_unit_text(const AesArgs& a, uint64_t gq, ui
         const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
         R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
       }
-      b64_coalesce(R);
-      if (a.skew != 0u) {
-        uint32_t e[4];
-        if (lane == 63u) {
-          const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 4096));
-          e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
-          R[16 + i] = lane == 63u ? e[i] : nx;
-        }
+      if (a.skew != 0u) {  // the next wave's first chunk (lane 63's; every lane loads the line)
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 4096));
+        R[16] = x.x, R[17] = x.y, R[18] = x.z, R[19] = x.w;
       }
-      return;
+      return 1u;
     }
   }
   if constexpr (HEX && DN_AES_DEC_COAL) {
-    if (__ballot(1) == ~0ull) {
+    if (WHOLE || __ballot(1) == ~0ull) {
       const uint64_t w0 = tb * (gq - lane);
 #if DN_AES_DEC_COAL == 2
       // half lines (hex_coalesce_half, the encrypt's default transpose, also its own inverse)
@@ -1095,7 +1086,6 @@ __device__ __forceinline__ void load_unit_text(const AesArgs& a, uint64_t gq, ui
         const u32x4 x = __builtin_nontemporal_load(p + 128 * (v & 1) + 256 * ((v >> 1) & 1) + 4 * (v >> 2));
         R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
       }
-      hex_coalesce_half(R);
 #else
       const u32x4* p = reinterpret_cast<const u32x4*>(a.in + w0 + 128 * (lane & 7u) + 16 * (lane >> 3));
 #pragma unroll
@@ -1103,24 +1093,47 @@ __device__ __forceinline__ void load_unit_text(const AesArgs& a, uint64_t gq, ui
         const u32x4 x = __builtin_nontemporal_load(p + 64 * v);
         R[4 * v] = x.x, R[4 * v + 1] = x.y, R[4 * v + 2] = x.z, R[4 * v + 3] = x.w;
       }
-      hex_coalesce(R, lane);
 #endif
-      if (a.skew != 0u) {
-        uint32_t e[4];
-        if (lane == 63u) {
-          const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 8192));
-          e[0] = x.x, e[1] = x.y, e[2] = x.z, e[3] = x.w;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
-          R[32 + i] = lane == 63u ? e[i] : nx;
-        }
+      if (a.skew != 0u) {  // lane 63's next chunk: every lane loads it (one line; no exec-masked load,
+                           // whose conditional count made the loop's first wait vmcnt(0))
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.in + w0 + 8192));
+        R[32] = x.x, R[33] = x.y, R[34] = x.z, R[35] = x.w;
       }
-      return;
+      return 1u;
     }
   }
   load_raw<NV>(a.in, a.skew, tb * gq, R);
+  return 0u;
+}
+
+template <bool HEX>
+__device__ __forceinline__ void finish_unit_text(const AesArgs& a, uint32_t lane, uint32_t mode,
+                                                 uint32_t (&R)[HEX ? 36 : 20]) {
+  if (!mode) return;  // each lane loaded its own unit (shift_raw aligns it)
+  constexpr int NV = HEX ? 8 : 4;
+  if constexpr (HEX) {
+#if DN_AES_DEC_COAL == 2
+    hex_coalesce_half(R);
+#else
+    hex_coalesce(R, lane);
+#endif
+  } else {
+    b64_coalesce(R);
+  }
+  if (a.skew != 0u) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t nx = static_cast<uint32_t>(__shfl_down(static_cast<int>(R[i]), 1));
+      R[4 * NV + i] = lane == 63u ? R[4 * NV + i] : nx;
+    }
+  }
+}
+
+template <bool HEX>
+__device__ __forceinline__ void load_unit_text(const AesArgs& a, uint64_t gq, uint32_t lane,
+                                             uint32_t (&R)[HEX ? 36 : 20]) {
+  const uint32_t mode = issue_unit_text<HEX>(a, gq, lane, R);
+  finish_unit_text<HEX>(a, lane, mode, R);
 }
 
 template <bool HEX>
@@ -1211,37 +1224,49 @@ __global__ void __launch_bounds__(NTAB == 4 ? 1024 : 512) ctr_text_kernel(const 
   }
 }
 
-// One pass again (DN_AES_DEC_SPLIT == 2): decode_kernel's coalesced,
-// transposed text reads (the next unit's loaded before this unit's AES) and
-// its decode, then the unit's three keystream blocks and one store of the
-// plaintext — no ciphertext round trip through HBM.
+// One pass (DN_AES_DEC_SPLIT == 2): decode_kernel's coalesced, transposed
+// text reads and its decode, then the unit's three keystream blocks, each
+// block's plaintext stored as soon as its keystream is done — no ciphertext
+// round trip through HBM.  Round 6: units 0 and last (the nonce, the
+// padding: byte-wise) go to the first two threads, so the loop covers only
+// whole units 1 .. units - 2 (32-bit indices: the host keeps units < 2^32);
+// the nonce and padding, identical in every lane, are scalars; the next
+// unit's text loads are issued before this unit's AES and transposed only when
+// the next iteration needs them (issue_unit_text / finish_unit_text).  Round
+// 5's kernel spilled three 64-bit values whose reloads' vmcnt(0), and the
+// transpose inside the load, waited for those loads at once, exposing every
+// unit's text latency; this one carries no spill (118 VGPRs).
 template <int NR, bool HEX>
 __global__ void __launch_bounds__(1024) decrypt_fused_kernel(const AesArgs a) {
   __shared__ AesLds<4> L;
   build_tables<4>(L);
   const uint32_t lb = (threadIdx.x & 31u) << 2;
   const uint32_t lw[2] = {lb, lb | 0x10000u};
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 1024u;
-  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * 1024u + threadIdx.x;
   uint32_t iv[4];
   uint64_t pad;
   text_header<HEX>(a, L.dec, iv, pad);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) iv[k] = __builtin_amdgcn_readfirstlane(iv[k]);
+  pad = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(pad));
   const uint64_t nout = a.n / 4 * 3 - pad - 16;
-  if (first == 0) *a.out_len = nout;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.out_len = nout;
   constexpr int NV = HEX ? 8 : 4;
   uint32_t R[4 * NV + 4];
-  auto whole = [&](uint64_t g) { return g != 0 && g + 1 < a.units; };
   const uint32_t lane = threadIdx.x & 63u;
-  if (first < a.units && whole(first)) load_unit_text<HEX>(a, first, lane, R);
-  for (uint64_t g = first; g < a.units; g += stride) {
-    const uint64_t gn = g + stride;
-    if (!whole(g)) {
-      decrypt_unit_slow<NR, 4, HEX>(L, lw, a, iv, g, pad, nout);
-      if (gn < a.units && whole(gn)) load_unit_text<HEX>(a, gn, lane, R);
-      continue;
-    }
+  if (blockIdx.x == 0 && threadIdx.x < 2u) {
+    const uint64_t gs = threadIdx.x ? a.units - 1 : 0;
+    if (threadIdx.x == 0u || a.units > 1) decrypt_unit_slow<NR, 4, HEX>(L, lw, a, iv, gs, pad, nout);
+  }
+  const uint32_t last = static_cast<uint32_t>(a.units) - 1u;  // whole units: 1 .. last - 1
+  const uint32_t stride = gridDim.x * 1024u;
+  const uint32_t first = 1u + blockIdx.x * 1024u + threadIdx.x;
+  uint32_t mode = 0u;  // how R's loads were issued (finish_unit_text)
+  if (a.units >= 3 && first < last) mode = issue_unit_text<HEX>(a, first, lane, R);
+  for (uint32_t g = first; a.units >= 3 && g < last; g += stride) {
+    const uint32_t gn = g + stride;
     uint32_t T[16], bad = 0u;
     {
+      finish_unit_text<HEX>(a, lane, mode, R);  // this unit's text, loaded one unit ago
       uint32_t tx[4 * NV];
       shift_raw<NV>(R, a.skew, tx);
       if constexpr (HEX) {
@@ -1252,27 +1277,22 @@ __global__ void __launch_bounds__(1024) decrypt_fused_kernel(const AesArgs a) {
         for (int k = 0; k < 16; ++k) T[k] = tx[k];
       }
     }
-    if (gn < a.units && whole(gn)) load_unit_text<HEX>(a, gn, lane, R);  // the next unit's text, ahead
+    if (gn < last) mode = issue_unit_text<HEX>(a, gn, lane, R);  // in flight across the AES
     uint32_t x[16], acc = 0u;
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = unb64_word(L.dec, T[k], acc);
     if ((acc & (kDecPad | kDecBad)) | bad) atomicOr(a.bad, 1u);
     uint32_t W[12];
     join24(x, W);
-    uint32_t ks[3][4];
+    uint8_t* o = a.out + 48 * static_cast<uint64_t>(g) - 16;  // plaintext of keystream blocks 3g-1 .. 3g+1
 #pragma unroll
-    for (int j = 0; j < 3; ++j) ctr_block(iv, 3 * g - 1 + j, ks[j]);
-#if DN_AES_DEC_NB == 3
-    aes_blocks<NR, 3>(L, lw, a, ks);
-#else
-#pragma unroll
-    for (int j = 0; j < 3; ++j) aes_block<NR>(L, lw, a, ks[j]);
-#endif
-    uint8_t* o = a.out + 48 * g - 16;  // plaintext bytes of keystream blocks 3g-1 .. 3g+1
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      store4(o + 16 * j, __builtin_bswap32(W[4 * j] ^ ks[j][0]), __builtin_bswap32(W[4 * j + 1] ^ ks[j][1]),
-             __builtin_bswap32(W[4 * j + 2] ^ ks[j][2]), __builtin_bswap32(W[4 * j + 3] ^ ks[j][3]));
+    for (int j = 0; j < 3; ++j) {  // each block stored as soon as its keystream is done
+      uint32_t ks[4];
+      ctr_block(iv, 3 * static_cast<uint64_t>(g) - 1 + j, ks);
+      aes_block<NR>(L, lw, a, ks);
+      store4(o + 16 * j, __builtin_bswap32(W[4 * j] ^ ks[0]), __builtin_bswap32(W[4 * j + 1] ^ ks[1]),
+             __builtin_bswap32(W[4 * j + 2] ^ ks[2]), __builtin_bswap32(W[4 * j + 3] ^ ks[3]));
+    }
   }
 }
 
@@ -1516,6 +1536,9 @@ extern "C" int dn_aes_decrypt(const uint8_t* key, int key_bytes, const void* tex
   if (rc != DN_OK) return rc;
   a.n = hex ? n_text / 2 : n_text;
   a.units = (a.n + 63) / 64;
+  if (a.units >= (1ull << 32))  // decrypt_fused_kernel's 32-bit unit indices (256 GB of base64)
+    return set_error(DN_ERR_UNSUPPORTED, "dn_aes_decrypt: %llu characters exceed one launch",
+                     static_cast<unsigned long long>(n_text));
   a.out_len = out_len;
   a.bad = bad;
   hipStream_t s = static_cast<hipStream_t>(stream);
