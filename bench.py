@@ -1358,6 +1358,9 @@ def main():
     ceiling = recon_ceiling = None
     if N >= (1 << 20):
         fr = [split_bytes / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS for ms in split_by_buf]
+        # the same split into blocks a caller allocates (before the ceiling
+        # probes, which overwrite the timed blocks: the equality check needs them)
+        caller = caller_blocks_row(sec, coeffs, N, t, n, nbuf, stream, split_bytes, shares) if world == 1 else None
         ceils = [measure_ceiling(dev, sec, coeffs, share_bufs[b], N, t, n) for b in range(len(split_by_buf))]
         placement = {"buffers": len(split_by_buf), "steps_per_buffer": args.steps // max(1, nbuf),
                      "split_ms": split_by_buf, "frac": fr, "frac_min": min(fr), "frac_median": float(np.median(fr)),
@@ -1371,9 +1374,8 @@ def main():
         ceiling = {"ms": float(np.mean([c["ms"] for c in ceils])), "grid": [c["grid"] for c in ceils],
                    "kernel": ceils[0]["kernel"], "buffers": len(ceils)}
         recon_ceiling = measure_recon_ceiling(share_rows, rec, N)
-        if world == 1:
-            placement["caller_blocks"] = caller_blocks_row(sec, coeffs, N, t, n, nbuf, stream, split_bytes,
-                                                           shares)
+        if caller:
+            placement["caller_blocks"] = caller
     del share_bufs, row_sets
 
     # ---- N > 1: the weak-scaling figure (2^log2n elements per GPU) --------

@@ -99,9 +99,12 @@ PROBE_FIRST_SMALL = 4
 PROBE_FAST = 6.8e12            # the first block of a class keeps at once at this tiled-probe rate (B/s)
 PROBE_BUDGET = 48 << 30        # most bytes mapped at once for one request's tries (and
                                # never more than the device has free beyond POOL_MIN_FREE)
-# most wall time one request spends on tries after its first (mapping a 5.5 GB
-# block of 16 MiB chunks ~7.5 ms, its probe ~3 ms; freeing rejected ones): the
-# worst case, every try slow, stays ~50-60 ms instead of PROBE_TRIES tries
+# most wall time one request spends on its tries AND on freeing the tries it
+# rejects (a 5.5 GB block of 16 MiB chunks: ~3-7 ms to map, ~3 ms to probe,
+# ~5 ms to free): a request stops trying once the tries so far plus the
+# frees they imply (each at the measured cost of a free of that size) pass it,
+# so the worst case, every try slow, stays near this instead of PROBE_TRIES
+# tries and their frees (bench rows.draw_split.cold.cold_worst_ms)
 PROBE_TIME_BUDGET = 0.05
 # virtual address space that freed blocks may retire before new share blocks
 # come from torch.empty instead (x86-64 user space: 2^47 bytes)
@@ -115,6 +118,8 @@ _stats = {"allocs": 0, "reuses": 0, "frees": 0, "probed": 0, "rejected": 0, "wai
           "trimmed": 0, "record_failures": 0, "free_failures": 0, "budget_stops": 0, "va_fallbacks": 0}
 _best_rate: Dict[Tuple[int, int, int], float] = {}  # (device, rows, log2 bytes) -> fastest probed write rate (B/s)
 _rates: Dict[int, float] = {}      # block pointer -> its probed write rate
+_sizes: Dict[int, int] = {}        # block pointer -> its bytes (dn_block_alloc blocks of this module)
+_free_secs: Dict[int, float] = {}  # block bytes -> seconds one dn_block_free of that size took (last measured)
 _live: Dict[int, "weakref.ref"] = {}  # block pointer -> its live _Block (record_stream)
 _observer = False
 
@@ -132,8 +137,12 @@ def _free_ptr(ptr: int, streams: Sequence[int] = ()) -> None:
     L = _native.lib()
     for s in streams:
         _native.check(L.dn_block_record(ptr, s or None))
+    t0 = time.perf_counter()
     if L.dn_block_free(ptr):
         _stats["free_failures"] += 1
+    nbytes = _sizes.pop(ptr, None)
+    if nbytes:
+        _free_secs[nbytes] = time.perf_counter() - t0
     _stats["frees"] += 1
 
 
@@ -283,6 +292,7 @@ def _alloc_raw(nbytes: int, chunk_bytes: int, index: int) -> int:
         rc = _native.lib().dn_block_alloc(nbytes, int(chunk_bytes), index, ctypes.byref(p))
     _native.check(rc)
     _stats["allocs"] += 1
+    _sizes[p.value] = int(nbytes)
     return p.value
 
 
@@ -355,9 +365,15 @@ def _alloc_probed(nbytes: int, chunk_bytes: int, dev, shape) -> int:
                 break
         elif rate >= PROBE_KEEP * best:
             break
-        if k + 1 < tries and time.perf_counter() - t0 > PROBE_TIME_BUDGET:
-            _stats["budget_stops"] += 1  # out of time for this request: keep the best so far
-            break
+        if k + 1 < tries:
+            # the tries so far, one more, and the frees of all but the kept one
+            # (each at the last measured free of this size, else a try's cost)
+            spent = time.perf_counter() - t0
+            per_try = spent / (k + 1)
+            free_cost = _free_secs.get(nbytes, per_try)
+            if spent + per_try + (k + 1) * free_cost > PROBE_TIME_BUDGET:
+                _stats["budget_stops"] += 1  # out of time for this request: keep the best so far
+                break
     rate, keep = max(cands)
     stream = _current_stream(dev.index)  # the probe wrote the rejected blocks on this stream
     for r, p in cands:

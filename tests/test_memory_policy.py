@@ -299,16 +299,26 @@ def test_failed_record_frees_the_block_after_a_device_wait(pool):
 
 
 def test_time_budget_stops_the_tries(fake, monkeypatch):
-    """Every try slow: the request stops once PROBE_TIME_BUDGET has passed and
-    keeps the best block so far (the cold worst case stays bounded)."""
+    """Every try slow: the request stops once its tries plus the frees they
+    imply (at the measured free cost of that size) would pass
+    PROBE_TIME_BUDGET, and keeps the best block so far (the cold worst case
+    stays bounded)."""
     f = fake([7.0, 6.0] + [5.0, 5.1, 5.2, 5.3, 5.4, 5.5, 5.6, 5.7] + [9.9])
     memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # best 7.0
-    clock = iter([0.0] + [0.02 * k for k in range(1, 100)])  # each try takes 20 ms
+    monkeypatch.setattr(memory, "_free_secs", {NBIG: 0.010})  # a free of this size took 10 ms
+    clock = iter([0.0] + [0.005 * k for k in range(1, 100)])  # each try takes 5 ms
     monkeypatch.setattr(memory.time, "perf_counter", lambda: next(clock))
     before = memory._stats["budget_stops"]
     p = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)
-    # tries at 20 / 40 / 60 ms: the third ends past the 50 ms budget
-    assert f.rate_of[p] == 5.2 and f.rates[0] == 5.3 and memory._stats["budget_stops"] == before + 1
+    # after try k (k = 1..): 5k ms spent + 5 ms next + 10k ms of frees; k = 4 passes 50 ms
+    assert f.rate_of[p] == 5.3 and f.rates[0] == 5.4 and memory._stats["budget_stops"] == before + 1
+    g = fake([7.0, 6.0] + [5.0, 5.1, 5.2] + [9.9])  # no free measured yet: a free costs a try
+    memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)
+    monkeypatch.setattr(memory, "_free_secs", {})
+    clock2 = iter([0.0] + [0.02 * k for k in range(1, 100)])  # 20 ms tries
+    monkeypatch.setattr(memory.time, "perf_counter", lambda: next(clock2))
+    q = memory._alloc_probed(NBIG, 2 << 20, DEV, BIG)  # 20 + 20 + 20 > 50 after the first
+    assert g.rate_of[q] == 5.0 and g.rates[0] == 5.1
 
 
 def test_retire_budget_limits_the_tries(fake, monkeypatch):
