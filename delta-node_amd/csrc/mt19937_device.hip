@@ -141,6 +141,15 @@ struct JumpJob {
 #define DN_MT_RT_DIRECT 1
 #endif
 
+// DN_MT_SPLIT2: the 2^24 draw's direct level in two halves; the first half's
+// generation (substreams [0, S/2), on a side stream) runs while the second
+// half's jumps do (their 85 KB tables beside the generation's rings), then the
+// second half's generation (round 6; the tuning build's env knob of the same
+// name A/Bs it).
+#ifndef DN_MT_SPLIT2
+#define DN_MT_SPLIT2 0
+#endif
+
 // A latency-bound level (few jobs: one Horner chain of ~312 steps per jump)
 // splits every jump into P parts over word ranges [lo, hi) of g.  Since
 // g(f) W = sum_k f^(64 k) g_k(f) W, part [lo, hi) evaluates
@@ -458,6 +467,8 @@ struct GenArgs {
   uint32_t ring;         // ring slots of one wave (2 emission groups; GenRing)
   uint32_t back;         // even substreams 2 .. S-2 run backward from the next window
   uint32_t probe;        // tuning build only (DN_MT_PROBE): 1 skip emissions, 2 skip generation
+  uint32_t sub_lo;       // substream of workgroup 0 (a launch over substreams sub_lo ..: DN_MT_SPLIT2)
+  uint32_t sub_n;        // workgroups of the launch (0: S + 1, every substream and the final-state wave)
 };
 
 // DN_MT_PROBE (tuning build): time the generation and the emission apart.
@@ -793,7 +804,7 @@ template <int T, int SAUX = kNt, int NS = 0>
 __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t sub = blockIdx.x;
+  const uint32_t sub = blockIdx.x + a.sub_lo;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
   const bool fin_wave = sub == a.S;
   const bool fwd = fin_wave || mt_sub_forward(sub, a.S, static_cast<int>(a.back));
@@ -973,7 +984,7 @@ __global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const Ge
   const uint32_t lane = threadIdx.x & 63u;
   // (roles alternating with the workgroup's parity: no faster, profiles/r04/l/)
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 consumer, 1 producer
-  const uint32_t sub = blockIdx.x;
+  const uint32_t sub = blockIdx.x + a.sub_lo;
   if (sub > a.S || (sub == a.S && a.final_sig < 0)) return;
   const bool fin_wave = sub == a.S;
   const bool fwd = fin_wave || mt_sub_forward(sub, a.S, static_cast<int>(a.back));
@@ -1212,11 +1223,12 @@ std::vector<int32_t> part_cuts(int P, int W) {
 }
 
 void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs,
-                int32_t prow0) {
+                int32_t prow0, int p_force = 0) {
   size_t n = 0, most = 0;  // jumps, and the most of one source
   for (auto& sp : srcs) n += sp.second.size(), most = std::max(most, sp.second.size());
   if (n == 0) return;
   int P = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kMaxParts, kPartRows / n)));
+  if (p_force > 0) P = std::min(p_force, kMaxParts);
   // DN_MT_PARTS_B (tuning build): the part count of levels of 256 jumps or more
   const char* pb = n >= 256 ? tune_env("DN_MT_PARTS_B") : nullptr;
   if (pb && std::atoi(pb) >= 1) P = std::min(kMaxParts, std::atoi(pb));
@@ -1257,11 +1269,27 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
 // draws of up to kMtRtRows + 1 substreams of 2^14 draws that generate
 // backward: the 1024 windows of a 2^24-element 3-of-5 draw in one level of
 // ~150 us instead of level A (~28 us), its combine and level B (~148 us).
-void build_levels(uint64_t S, int ki, int back, bool rt, Level lv[3]) {
+// split2 (DN_MT_SPLIT2): the runtime direct level as two levels, the windows
+// of substreams [0, S/2) and of [S/2, S), at the whole level's part count, so
+// the first half's generation can start while the second half's jumps run.
+void build_levels(uint64_t S, int ki, int back, bool rt, Level lv[3], bool split2 = false) {
   const uint64_t R = kMtJumpRadix;
   if (S < 2) return;
   const uint64_t last = S - 2;  // largest s - 1
   const int32_t prow0 = static_cast<int32_t>(S + 1);
+  if (rt && split2) {
+    const uint64_t half = S / 2;
+    std::vector<std::pair<int32_t, int32_t>> pd1, pd2;
+    for (uint64_t s = 1; s < S; ++s)
+      if (mt_window_needed(static_cast<uint32_t>(s), S, back))
+        (s < half ? pd1 : pd2).push_back({kMtRtBase + static_cast<int32_t>(s - 1), static_cast<int32_t>(s)});
+    const int P = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kMaxParts, kPartRows / (pd1.size() + pd2.size()))));
+    push_level(lv[0], {{-1, pd1}}, prow0, P);
+    int32_t prow1 = prow0;
+    for (auto& c : lv[0].comb) prow1 = std::max(prow1, c.first + c.parts);
+    push_level(lv[1], {{-1, pd2}}, prow1, P);
+    return;
+  }
   if (rt) {
     std::vector<std::pair<int32_t, int32_t>> pd;
     for (uint64_t s = 1; s < S; ++s)
@@ -1318,6 +1346,7 @@ struct MtHost {
   int back = 0;
   int parts_b = 0;  // tuning build: DN_MT_PARTS_B the levels were built with
   bool rt = false;  // one direct level through the runtime rows
+  bool split2 = false;  // that level in two halves (DN_MT_SPLIT2)
   Level lv[3];
   std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
@@ -1346,9 +1375,11 @@ MtHost& mt_levels(uint64_t S, int ki) {
   const bool rt = DN_MT_RT_DIRECT && !(rte && rte[0] == '0') && ki == 2 && back == 1 &&
                   S - 1 > static_cast<uint64_t>(kMtDirectRows) && S - 1 <= kMtRtRows &&
                   mt_direct_rows_l14(S, nullptr) != nullptr;
-  if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b || H.rt != rt) {
+  const char* sp = tune_env("DN_MT_SPLIT2");
+  const bool split2 = rt && (sp ? sp[0] == '1' : DN_MT_SPLIT2 != 0) && S >= 4 && S % 2 == 0;
+  if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b || H.rt != rt || H.split2 != split2) {
     for (auto& l : H.lv) l = Level();
-    build_levels(S, ki, back, rt, H.lv);
+    build_levels(S, ki, back, rt, H.lv, split2);
     uint64_t nj = 0, nc = 0;
     for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
     H.part_rows = 0;
@@ -1369,6 +1400,7 @@ MtHost& mt_levels(uint64_t S, int ki) {
     H.back = back;
     H.parts_b = parts_b;
     H.rt = rt;
+    H.split2 = split2;
   }
   return H;
 }
@@ -1442,7 +1474,7 @@ struct DevJobs {
   int dev;
   uint64_t S;
   int ki, back, parts_b;
-  bool rt;
+  bool rt, split2;
   void* p;
 };
 
@@ -1456,7 +1488,8 @@ const void* device_jobs(const MtHost& H, int* err) {
   }
   std::lock_guard<std::mutex> g(*m);
   for (const DevJobs& d : *cache)
-    if (d.dev == dev && d.S == H.S && d.ki == H.ki && d.back == H.back && d.parts_b == H.parts_b && d.rt == H.rt)
+    if (d.dev == dev && d.S == H.S && d.ki == H.ki && d.back == H.back && d.parts_b == H.parts_b && d.rt == H.rt &&
+        d.split2 == H.split2)
       return d.p;
   void* p = nullptr;
   const size_t bytes = std::max<size_t>(H.jobs.size() * 4, 16);
@@ -1466,7 +1499,7 @@ const void* device_jobs(const MtHost& H, int* err) {
     *err = 1;
     return nullptr;
   }
-  cache->push_back({dev, H.S, H.ki, H.back, H.parts_b, H.rt, p});
+  cache->push_back({dev, H.S, H.ki, H.back, H.parts_b, H.rt, H.split2, p});
   return p;
 }
 
@@ -1522,6 +1555,28 @@ const uint64_t* device_rt(uint64_t S, int* err) {
 #ifndef DN_MT_SPIN_SYNC
 #define DN_MT_SPIN_SYNC 0
 #endif
+// DN_MT_SPLIT2's side stream and its two events, per thread and device
+// (created once, never destroyed: the runtime may be torn down first).
+struct SideStream {
+  int dev = -1;
+  hipStream_t s = nullptr;
+  hipEvent_t levels = nullptr, gen = nullptr;
+};
+SideStream* side_stream() {
+  thread_local SideStream side[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  SideStream& x = side[dev];
+  if (!x.s) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return x.s = nullptr, nullptr;
+    if (hipEventCreateWithFlags(&x.levels, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.gen, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+    x.dev = dev;
+  }
+  return &x;
+}
+
 hipError_t mt_wait(hipStream_t s) {
 #if DN_MT_SPIN_SYNC
   thread_local hipEvent_t ev = nullptr;
@@ -1624,6 +1679,11 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     (void)hipStreamSynchronize(s);  // the staging buffer is reused by the next call
     return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   }
+  SideStream* side = H.split2 ? side_stream() : nullptr;
+  if (H.split2 && !side) {
+    (void)hipStreamSynchronize(s);
+    return set_error(DN_ERR_HIP, "%s: side stream", name);
+  }
   uint64_t off = 0, coff = 0;
   for (int k = 0; k < 3; ++k) {
     const Level& l = lv[k];
@@ -1640,6 +1700,8 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
                          dcomb + coff);
     off += l.jobs.size();
     coff += l.comb.size();
+    // split2: the first half's windows are complete after level 0
+    if (side && k == 0) err = hipEventRecord(side->levels, s);
   }
   GenArgs ga{};
   ga.wins = dwin;
@@ -1670,7 +1732,28 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   ga.back = static_cast<uint32_t>(H.back);
   const char* pr = tune_env("DN_MT_PROBE");
   ga.probe = pr ? static_cast<uint32_t>(std::atoi(pr)) : 0u;
-  launch_gen(ga, s);
+  if (side) {
+    // substreams [0, S/2) on the side stream once level 0 is done (beside
+    // level 1's jumps), then [S/2, S] and the final-state wave on the call's
+    // stream after level 1; the call's stream then waits for the side stream
+    const uint32_t half = static_cast<uint32_t>(S / 2);
+    if (err == hipSuccess) err = hipStreamWaitEvent(side->s, side->levels, 0);
+    GenArgs g1 = ga;
+    g1.sub_lo = 0u;
+    g1.sub_n = half;
+    launch_gen(g1, side->s);
+    if (err == hipSuccess) err = hipEventRecord(side->gen, side->s);
+    ga.sub_lo = half;
+    ga.sub_n = static_cast<uint32_t>(S) + 1u - half;
+    launch_gen(ga, s);
+    if (err == hipSuccess) err = hipStreamWaitEvent(s, side->gen, 0);
+  } else {
+    launch_gen(ga, s);
+  }
+  if (err != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    return set_error(DN_ERR_HIP, "%s: side stream: %s", name, hipGetErrorString(err));
+  }
   err = hipGetLastError();
   if (err != hipSuccess) {
     (void)hipStreamSynchronize(s);
@@ -1735,7 +1818,7 @@ void launch_gen(GenArgs& ga, hipStream_t s) {
     // DN_MT_GEN_SUBS (tuning build, timing probe only: the output is partial and
     // CPython's final state is not computed): launch only the first K substream
     // workgroups — how the generation's time scales with the substreams in flight
-    uint32_t grid = ga.S + 1;
+    uint32_t grid = ga.sub_n ? ga.sub_n : ga.S + 1;
     if (const char* gs = tune_env("DN_MT_GEN_SUBS")) grid = std::min<uint32_t>(grid, std::max(1, std::atoi(gs)));
     if (pc) {
       if (T == 3 && ga.n_shares == 5)
@@ -1745,10 +1828,11 @@ void launch_gen(GenArgs& ga, hipStream_t s) {
       return;
     }
   }
+  const dim3 g1(ga.sub_n ? ga.sub_n : ga.S + 1);
   if (T == 3 && ga.n_shares == 5)
-    hipLaunchKernelGGL((mt_gen_kernel<T, kSc1, T == 3 ? 5 : 0>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+    hipLaunchKernelGGL((mt_gen_kernel<T, kSc1, T == 3 ? 5 : 0>), g1, dim3(64), lds_words * 4u, s, ga);
   else
-    hipLaunchKernelGGL((mt_gen_kernel<T>), dim3(ga.S + 1), dim3(64), lds_words * 4u, s, ga);
+    hipLaunchKernelGGL((mt_gen_kernel<T>), g1, dim3(64), lds_words * 4u, s, ga);
 }
 
 }  // namespace

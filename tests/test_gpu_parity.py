@@ -638,3 +638,38 @@ def test_vector_split_rejects_out_off_the_device():
     want = torch.empty_like(got)
     _native.split_u64(vals.to(got.device), ref.draw_coeffs_vec(1024, got.device), want, 1024, 4, 6)
     assert torch.equal(got, want) and ss4.random.getstate() == ref.random.getstate()
+
+
+@pytest.mark.parametrize("N,t,n,pre", [(1 << 24, 3, 5, 0), (1 << 24, 3, 5, 333), (1 << 23, 5, 9, 7),
+                                       (1026 * 16384 - 5, 2, 3, 600)])
+def test_split2_draw_equals_host_draw(N, t, n, pre, monkeypatch):
+    """DN_MT_SPLIT2 (tuning build): the 2^24-scale draw's direct jump level in
+    two halves, the first half's generation on a side stream beside the second
+    half's jumps.  The fused split (and, for t = 3, the coefficient draw) equal
+    the host draw + split byte for byte with the same final random.Random
+    state — at 2048 substreams, from a mid-array start, and at S = 1026 with a
+    partial last substream."""
+    monkeypatch.setenv("DN_MT_SPLIT2", "1")
+    sec = torch.from_numpy(secrets_int64(N % 1000 + 3, N)).to(dev())
+    a, b = shamir.SecretShare(t), shamir.SecretShare(t)
+    a.random.seed(N + pre)
+    a.random.getrandbits(32 * pre)
+    b.random.setstate(a.random.getstate())
+    with _native.library(_native.TUNING_LIB):
+        out = torch.empty((n, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
+        assert _native.mt_split_device(a.random, sec, out, N, t, n)
+        co = torch.from_numpy(_native.mt_draw_coeffs(b.random, N, t - 1)).to(dev())
+        want = torch.empty_like(out)
+        _native.split_u64(sec, co, want, N, t, n)
+        if N % 256:
+            assert np.array_equal(block_limbs(out, N), block_limbs(want, N))  # (tile padding is never written)
+        else:
+            assert torch.equal(out, want)
+        assert a.random.getstate() == b.random.getstate()
+        if t == 3 and pre == 0:
+            c = random.Random(77)
+            d = random.Random(77)
+            got = torch.zeros((2, field.vec_bytes(N)), dtype=torch.uint8, device=dev())
+            assert _native.mt_draw_coeffs_device(c, N, 2, got)
+            assert torch.equal(got, torch.from_numpy(_native.mt_draw_coeffs(d, N, 2)).to(dev()))
+            assert c.getstate() == d.getstate()
