@@ -1269,6 +1269,11 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
 // draws of up to kMtRtRows + 1 substreams of 2^14 draws that generate
 // backward: the 1024 windows of a 2^24-element 3-of-5 draw in one level of
 // ~150 us instead of level A (~28 us), its combine and level B (~148 us).
+// The first substream of split2's second half: even, so the first half's
+// last substream (odd) runs forward from a window of the first half, and every
+// even substream runs backward from a window of its own half.
+inline uint64_t mt_split_half(uint64_t S) { return (S / 2 + 1) & ~1ull; }
+
 // split2 (DN_MT_SPLIT2): the runtime direct level as two levels, the windows
 // of substreams [0, S/2) and of [S/2, S), at the whole level's part count, so
 // the first half's generation can start while the second half's jumps run.
@@ -1278,7 +1283,7 @@ void build_levels(uint64_t S, int ki, int back, bool rt, Level lv[3], bool split
   const uint64_t last = S - 2;  // largest s - 1
   const int32_t prow0 = static_cast<int32_t>(S + 1);
   if (rt && split2) {
-    const uint64_t half = S / 2;
+    const uint64_t half = mt_split_half(S);
     std::vector<std::pair<int32_t, int32_t>> pd1, pd2;
     for (uint64_t s = 1; s < S; ++s)
       if (mt_window_needed(static_cast<uint32_t>(s), S, back))
@@ -1376,7 +1381,7 @@ MtHost& mt_levels(uint64_t S, int ki) {
                   S - 1 > static_cast<uint64_t>(kMtDirectRows) && S - 1 <= kMtRtRows &&
                   mt_direct_rows_l14(S, nullptr) != nullptr;
   const char* sp = tune_env("DN_MT_SPLIT2");
-  const bool split2 = rt && (sp ? sp[0] == '1' : DN_MT_SPLIT2 != 0) && S >= 4 && S % 2 == 0;
+  const bool split2 = rt && (sp ? sp[0] == '1' : DN_MT_SPLIT2 != 0) && S >= 4;
   if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b || H.rt != rt || H.split2 != split2) {
     for (auto& l : H.lv) l = Level();
     build_levels(S, ki, back, rt, H.lv, split2);
@@ -1736,7 +1741,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     // substreams [0, S/2) on the side stream once level 0 is done (beside
     // level 1's jumps), then [S/2, S] and the final-state wave on the call's
     // stream after level 1; the call's stream then waits for the side stream
-    const uint32_t half = static_cast<uint32_t>(S / 2);
+    const uint32_t half = static_cast<uint32_t>(mt_split_half(S));
     if (err == hipSuccess) err = hipStreamWaitEvent(side->s, side->levels, 0);
     GenArgs g1 = ga;
     g1.sub_lo = 0u;

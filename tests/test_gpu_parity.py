@@ -641,14 +641,15 @@ def test_vector_split_rejects_out_off_the_device():
 
 
 @pytest.mark.parametrize("N,t,n,pre", [(1 << 24, 3, 5, 0), (1 << 24, 3, 5, 333), (1 << 23, 5, 9, 7),
-                                       (1026 * 16384 - 5, 2, 3, 600)])
+                                       (1026 * 16384 - 5, 2, 3, 600), ((1 << 24) + 1, 2, 3, 0)])
 def test_split2_draw_equals_host_draw(N, t, n, pre, monkeypatch):
     """DN_MT_SPLIT2 (tuning build): the 2^24-scale draw's direct jump level in
     two halves, the first half's generation on a side stream beside the second
     half's jumps.  The fused split (and, for t = 3, the coefficient draw) equal
     the host draw + split byte for byte with the same final random.Random
-    state — at 2048 substreams, from a mid-array start, and at S = 1026 with a
-    partial last substream."""
+    state — at 2048 substreams, from a mid-array start, at S = 1026 with a
+    partial last substream (the halves split at an even substream: 514) and at
+    S = 1025 (an even last window)."""
     monkeypatch.setenv("DN_MT_SPLIT2", "1")
     sec = torch.from_numpy(secrets_int64(N % 1000 + 3, N)).to(dev())
     a, b = shamir.SecretShare(t), shamir.SecretShare(t)
