@@ -1475,6 +1475,10 @@ def main():
                         "reconstruct_frac_of_ceiling": recon_ceiling["ms"] / recon_ms}},
         "parity": {"roundtrip_equal": roundtrip, "c_oracle_sample_equal": oracle_ok, "sample": sample,
                    "reference_digest_equal": ref_digest_ok, "all_ranks_ok": all_ok},
+        # share blocks memory.share_block mapped, write-probed and freed to place
+        # this run's timed blocks (their fractions: roofline.placement; the same
+        # split on caller-allocated blocks: roofline.placement.caller_blocks)
+        "probe_rejected_blocks": placement and placement["pool"]["rejected"],
     }
     if weak:
         line["weak_scaling"] = weak
