@@ -963,6 +963,7 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
     # the product default (out=None: each call's block from memory.share_block,
     # the previous one back to the pool) and a caller's own torch.empty block
     loop = {}
+    spec0 = _native.mt_spec_stats()
     for name in ("pooled_default_out", "caller_out"):
         ss = shamir.SecretShare(3)
         ss.random.seed(91)
@@ -979,6 +980,12 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
         torch.cuda.synchronize()
         loop[name] = (time.perf_counter() - t0) / reps_l * 1e3
         del mine
+    spec1 = _native.mt_spec_stats()
+    # calls of the loops that used windows speculated by the call before
+    # (DN_MT_SPEC: a call continuing its predecessor computes the next one's
+    # jump levels on a side stream beside its generation)
+    loop["speculated_calls"] = spec1["hits"] - spec0["hits"]
+    loop["calls"] = 2 * (3 + 10)
     words = 17 * 2 * n
     # smaller vectors take shorter MT substreams (2^10 / 2^12 / 2^14 draws: dn_mt19937_split_device)
     by_size = {}

@@ -469,6 +469,13 @@ struct GenArgs {
   uint32_t probe;        // tuning build only (DN_MT_PROBE): 1 skip emissions, 2 skip generation
   uint32_t sub_lo;       // substream of workgroup 0 (a launch over substreams sub_lo ..: DN_MT_SPLIT2)
   uint32_t sub_n;        // workgroups of the launch (0: S + 1, every substream and the final-state wave)
+  uint32_t* next_win;    // the next call's W_idx (null: not wanted), written with the final state
+  uint64_t next_pos;     // its position idx + 17 ncoef (final-state wave)
+  // tail_fin: the last substream writes the final state (and next_win) itself
+  // after its generation, at positions fin_lo / next_lo of its own frame
+  // (position 0 its first output); no final-state wave is launched
+  uint32_t tail_fin;
+  int32_t fin_lo, next_lo;  // (fin_lo < 0: words of the substream's window, still in the ring)
 };
 
 // DN_MT_PROBE (tuning build): time the generation and the emission apart.
@@ -573,6 +580,62 @@ __device__ __forceinline__ void ring_batch(uint32_t* Rg, const GenRing& g, uint3
 }
 
 // NA appends as batches of three (one of one or two last).
+// The final-state wave: CPython's final array (stream positions tf .. tf +
+// 623) into a.fin, from the window at position P = a.final_pos (its word 0)
+// onwards, and — when the call speculates on its successor (a.next_win,
+// DN_MT_SPEC) — the window at position a.next_pos (>= tf): the next call's
+// W_idx, the source of its jump levels.
+__device__ __forceinline__ void final_state_wave(uint32_t* R, const GenRing& g, uint32_t slot, uint32_t lane,
+                                                 const uint32_t* win, const GenArgs& a) {
+  const uint64_t P = a.final_pos, tf = a.final_tf, nx = a.next_pos;
+  uint32_t* nw = a.next_win;
+  const uint64_t end = nw ? nx + kMtN : tf + kMtN;
+  for (uint32_t i = lane; i < static_cast<uint32_t>(kMtN); i += 64u) {
+    const uint64_t x = P + i;
+    if (x >= tf && x < tf + kMtN) a.fin[x - tf] = win[i];
+    if (nw && x >= nx && x < nx + kMtN) nw[x - nx] = win[i];
+  }
+  uint64_t np = P + kMtN;  // position of the next append's word 0
+  while (np < end) {
+    uint32_t v[3];
+    ring_batch<3>(R, g, slot, lane, v);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint64_t x = np + 64u * k + lane;
+      if (x >= tf && x < tf + kMtN) a.fin[x - tf] = v[k];
+      if (nw && x >= nx && x < nx + kMtN) nw[x - nx] = v[k];
+    }
+    np += 192u;
+  }
+}
+
+// The last substream's tail (tail_fin): CPython's final array (positions
+// fin_lo .. fin_lo + 623 of the substream's frame) and, when the call
+// speculates, the next call's W_idx (next_lo .., next_lo >= fin_lo), from the
+// ring — which holds the substream's last M words, `end` being the position
+// of the next append — and at most ten more appends.  The draw ends at
+// next_lo, at most 624 words past fin_lo and at most a group before `end`, so
+// every word needed is either still in the ring or appended here.
+__device__ __forceinline__ void last_sub_tail(uint32_t* R, const GenRing& g, uint32_t slot, uint32_t lane, uint32_t end,
+                                              const GenArgs& a) {
+  const int32_t f0 = a.fin_lo, n0 = a.next_lo, e = static_cast<int32_t>(end);
+  const int32_t off = static_cast<int32_t>(g.delta + g.M);  // slot of position x: (x + off) % M, x >= -624
+  uint32_t* nw = a.next_win;
+  for (int32_t i = static_cast<int32_t>(lane); i < kMtN; i += 64) {
+    const int32_t x = f0 + i, y = n0 + i;
+    if (x < e) a.fin[i] = R[g.o + static_cast<uint32_t>(x + off) % g.M];
+    if (nw && y < e) nw[i] = R[g.o + static_cast<uint32_t>(y + off) % g.M];
+  }
+  const int32_t stop = (nw ? n0 : f0) + kMtN;
+  for (int32_t p = e; p < stop; p += 64) {
+    uint32_t v[3];
+    ring_batch<1>(R, g, slot, lane, v);
+    const int32_t x = p + static_cast<int32_t>(lane);
+    if (x >= f0 && x < f0 + kMtN) a.fin[x - f0] = v[0];
+    if (nw && x >= n0 && x < n0 + kMtN) nw[x - n0] = v[0];
+  }
+}
+
 template <int NA>
 __device__ __forceinline__ void ring_run(uint32_t* Rg, const GenRing& g, uint32_t& slot, uint32_t lane) {
   uint32_t v[3];
@@ -826,22 +889,7 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
   uint32_t slot = __builtin_amdgcn_readfirstlane((p_start + g.delta) % g.M);  // slot of the next append
   wave_sync();
   if (fin_wave) {
-    // CPython's final array: positions tf .. tf + 623 of the whole stream,
-    // from the window at position P (its word 0) onwards
-    const uint64_t P = a.final_pos, tf = a.final_tf;
-    for (uint32_t i = lane; i < static_cast<uint32_t>(kMtN); i += 64u)
-      if (P + i >= tf && P + i < tf + kMtN) a.fin[P + i - tf] = win[i];
-    uint64_t np = P + kMtN;  // position of the next append's word 0
-    while (np < tf + kMtN) {
-      uint32_t v[3];
-      ring_batch<3>(R, g, slot, lane, v);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const uint64_t x = np + 64u * k + lane;
-        if (x >= tf && x < tf + kMtN) a.fin[x - tf] = v[k];
-      }
-      np += 192u;
-    }
+    final_state_wave(R, g, slot, lane, win, a);
     return;
   }
   const uint32_t group = a.ring / 2u;                            // words per emission group
@@ -911,6 +959,7 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
       emit_group(a, R + g.o + g.delta + (done & 1u) * group, qb, rbm, 64u * done + lane, nloc, lane);
       wave_sync();
     }
+    if (a.tail_fin && sub + 1u == a.S) last_sub_tail(R, g, slot, lane, p_start + ngroups * group, a);
   } else {
     // The int64 secret of this lane's element in the next group is loaded a
     // group ahead — before the current group's share stores, since loads and
@@ -959,6 +1008,10 @@ __global__ void __launch_bounds__(64) mt_gen_kernel(const GenArgs a) {
       emit_split<T, SAUX, NS, false>(a, R + g.o + g.delta + (gi & 1u) * group, qb + 64u * gi, lane, secret_of(gi));
     }
     asm volatile("" : : "v"(secA ^ secB));  // no load left in flight at the end
+    if (a.tail_fin && sub + 1u == a.S) {
+      wave_sync();
+      last_sub_tail(R, g, slot, lane, p_start + ngroups * group, a);
+    }
   }
 }
 
@@ -1002,20 +1055,7 @@ __global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const Ge
     if (wid != 0u) return;  // one wave steps to CPython's final array (as mt_gen_kernel)
     ring_init(R, g, win, p_start, lane);
     wave_sync();
-    const uint64_t P = a.final_pos, tf = a.final_tf;
-    for (uint32_t i = lane; i < static_cast<uint32_t>(kMtN); i += 64u)
-      if (P + i >= tf && P + i < tf + kMtN) a.fin[P + i - tf] = win[i];
-    uint64_t np = P + kMtN;
-    while (np < tf + kMtN) {
-      uint32_t v[3];
-      ring_batch<3>(R, g, slot, lane, v);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const uint64_t x = np + 64u * k + lane;
-        if (x >= tf && x < tf + kMtN) a.fin[x - tf] = v[k];
-      }
-      np += 192u;
-    }
+    final_state_wave(R, g, slot, lane, win, a);
     return;
   }
   const uint32_t group = a.ring / 2u;
@@ -1109,7 +1149,8 @@ __global__ void __launch_bounds__(128, T == 5 ? 2 : 4) mt_gen_pc_kernel(const Ge
       pc_barrier();
     }
     if (mid) pc_barrier();
-    pc_barrier();
+    pc_barrier();  // the consumer has read its last group: the ring is the producer's
+    if (a.tail_fin && sub + 1u == a.S) last_sub_tail(R, g, slot, lane, p_start + ngroups * group, a);
     return;
   }
   if constexpr (T == 0) {
@@ -1566,6 +1607,12 @@ struct SideStream {
   int dev = -1;
   hipStream_t s = nullptr;
   hipEvent_t levels = nullptr, gen = nullptr;
+  // DN_MT_SPEC_PROBE: the prefix copied, the side levels done (pending: a
+  // wait owed by the next call), the side levels' own buffer
+  hipEvent_t copy = nullptr, spec = nullptr;
+  bool pending = false;
+  void* buf = nullptr;
+  uint64_t buf_bytes = 0;
 };
 SideStream* side_stream() {
   thread_local SideStream side[16];
@@ -1575,11 +1622,97 @@ SideStream* side_stream() {
   if (!x.s) {
     if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return x.s = nullptr, nullptr;
     if (hipEventCreateWithFlags(&x.levels, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&x.gen, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&x.gen, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.copy, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.spec, hipEventDisableTiming) != hipSuccess)
       return nullptr;
     x.dev = dev;
   }
   return &x;
+}
+
+// DN_MT_SPEC (default 1; tuning build: DN_MT_SPEC=0 off): a call speculates
+// that the next draw on this device has the same size and starts where this
+// one ends — the loop `for x in batch: make_shares_vec(x)` — and computes the
+// next call's windows while its own host side finishes: the generation's last
+// substream also writes the next call's W_idx (the window at stream position
+// idx + 17 ncoef) into a buffer of the device's speculation state, then the
+// shape's jump levels from it run on a side stream into that buffer.  The
+// next call uses the buffer in place of its jump levels when its draw size,
+// CPython index and 624-word array equal the ones this call left (anything
+// else — another size, random.Random touched in between, a rejected draw —
+// is a miss: the call jumps itself).  A call speculates only when it
+// continues the previous call (same size, starting where that one ended), so
+// a lone call, or equal calls on fresh random.Random states, launch nothing
+// extra.  Two buffers alternate (one the generation reads, one the side
+// stream fills); the side stream's work is always awaited by the call stream
+// before a buffer is reused.  One state per device, process-wide; a call that
+// finds it busy (another thread's call) neither speculates nor hits.
+#ifndef DN_MT_SPEC
+#define DN_MT_SPEC 1
+#endif
+// The final state by the last substream (tail_fin, last_sub_tail) rather than
+// a final-state wave: that wave stepped the whole last substream again, one
+// wave alone, and finished ~100 us after the other substreams at 2^24
+// (profiles/r06/g/timeline_spec.json: substreams 0.88-0.91 ms, the wave
+// 0.93-1.09 ms).
+#ifndef DN_MT_TAIL_FIN
+#define DN_MT_TAIL_FIN 1
+#endif
+// draws of fewer coefficients than this do not speculate (tuning build: DN_MT_SPEC_MIN)
+#ifndef DN_MT_SPEC_MIN
+#define DN_MT_SPEC_MIN (1ull << 23)
+#endif
+struct SpecState {
+  std::mutex m;
+  hipStream_t side = nullptr;
+  hipEvent_t win = nullptr, done = nullptr;  // the next call's W_idx written (call stream), its levels done
+  void* buf[2] = {nullptr, nullptr};
+  uint64_t bytes = 0;  // of each buffer
+  bool armed = false;  // buf[next] holds (at `done`) the windows of a call starting as below
+  int next = 0;
+  uint64_t ncoef = 0;
+  int32_t idx = -1;
+  uint32_t state[kMtN];
+  bool have_end = false;  // ncoef, idx, state: where the previous call ended
+  uint64_t hits = 0, misses = 0, launched = 0;
+};
+
+std::mutex& spec_table_mutex() {
+  static std::mutex* m = new std::mutex;
+  return *m;
+}
+SpecState* spec_slot(int dev) {  // created once per device, never destroyed (the runtime may go first)
+  static SpecState* table[16] = {};
+  if (dev < 0 || dev >= 16) return nullptr;
+  std::lock_guard<std::mutex> g(spec_table_mutex());
+  if (!table[dev]) {
+    auto* x = new SpecState;
+    if (hipStreamCreateWithFlags(&x->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&x->win, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess)
+      return nullptr;  // (leaks the half-made state: a runtime that cannot make a stream has bigger problems)
+    table[dev] = x;
+  }
+  return table[dev];
+}
+
+// both buffers at least `need` bytes (false: allocation failed; no speculation)
+bool spec_buffers(SpecState& sp, uint64_t need) {
+  if (sp.bytes >= need && sp.buf[0] && sp.buf[1]) return true;
+  (void)hipStreamSynchronize(sp.side);  // nothing of ours uses them once the side stream is idle
+  sp.armed = false;
+  for (void*& b : sp.buf)
+    if (b) (void)hipFree(b), b = nullptr;
+  sp.bytes = 0;
+  for (void*& b : sp.buf)
+    if (hipMalloc(&b, need) != hipSuccess) {
+      for (void*& c : sp.buf)
+        if (c) (void)hipFree(c), c = nullptr;
+      return false;
+    }
+  sp.bytes = need;
+  return true;
 }
 
 hipError_t mt_wait(hipStream_t s) {
@@ -1675,38 +1808,106 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   mt_advance_window(mt_state, static_cast<uint64_t>(idx), stw);  // W_idx
   std::memcpy(stw + kMtN, mt_state, kMtN * 4);                    // row 0
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint8_t* sc = static_cast<uint8_t*>(scratch);
+  // DN_MT_SPEC_PROBE (tuning build, timing probe only: the output is wrong):
+  // 1 = the call's jump levels skipped (the generation reads stale windows);
+  // 2 = skipped, and the same levels run on the side stream into a buffer of
+  // their own, launched before the generation and awaited by the next call's
+  // generation — the cost of a next call's speculative levels beside this
+  // call's generation; 3 = as 2, launched after the generation.
+  const char* spp = tune_env("DN_MT_SPEC_PROBE");
+  const int spec_probe = spp ? std::atoi(spp) : 0;
+  // the speculation state (DN_MT_SPEC): this call's draw may have been
+  // speculated (hit), and it may speculate on the next one (spec_next)
+  const char* spe = tune_env("DN_MT_SPEC");
+  // DN_MT_TAIL_FIN (default 1; tuning build: 0 = the final-state wave)
+  const char* tfe = tune_env("DN_MT_TAIL_FIN");
+  const bool tail_fin = sig >= 0 && (tfe ? tfe[0] != '0' : DN_MT_TAIL_FIN != 0);
+  const char* spm = tune_env("DN_MT_SPEC_MIN");
+  const uint64_t spec_min = spm ? std::strtoull(spm, nullptr, 10) : DN_MT_SPEC_MIN;
+  const bool spec_on = (spe ? spe[0] != '0' : DN_MT_SPEC != 0) && spec_probe == 0 && !H.split2 && tail_fin &&
+                       njobs > 0 && ncoef >= spec_min;
+  SpecState* sp = nullptr;
+  std::unique_lock<std::mutex> spl;
+  if (spec_on) {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && (sp = spec_slot(dev))) {
+      spl = std::unique_lock<std::mutex>(sp->m, std::try_to_lock);
+      if (!spl.owns_lock()) sp = nullptr;
+    }
+  }
+  bool hit = false, spec_next = false;
+  if (sp) {
+    // this call continues the previous one (same size, starting where it
+    // ended): a hit if that call speculated, and a reason to speculate again
+    const bool cont = sp->have_end && sp->ncoef == ncoef && sp->idx == idx &&
+                      !std::memcmp(sp->state, mt_state, kMtN * 4);
+    hit = cont && sp->armed;
+    if (sp->armed && !hit) ++sp->misses;
+    sp->armed = false;
+    sp->have_end = false;
+    spec_next = cont && spec_buffers(*sp, dn_mt19937_device_scratch_bytes(n_elem, tm1));
+  }
+  const int spec_dst = sp ? sp->next ^ 1 : 0;  // the buffer the next call's windows go to
+  uint8_t* sc = hit ? static_cast<uint8_t*>(sp->buf[sp->next]) : static_cast<uint8_t*>(scratch);
   const JumpJob* djobs = static_cast<const JumpJob*>(jobs_dev);
   const CombineJob* dcomb = reinterpret_cast<const CombineJob*>(djobs + njobs);
   uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead) + kMtN;  // row 0
-  hipError_t err = hipMemcpyAsync(sc, pin, wpre * 4, hipMemcpyHostToDevice, s);
+  // the side stream's last work (the speculated levels) is done before this
+  // call writes a speculation buffer or reads one (a wait on the device only
+  // if it is still running)
+  hipError_t err = (spec_next || hit) && hipEventQuery(sp->done) != hipSuccess ? hipStreamWaitEvent(s, sp->done, 0)
+                                                                              : hipSuccess;
+  if (err == hipSuccess) err = hipMemcpyAsync(sc, pin, wpre * 4, hipMemcpyHostToDevice, s);
   if (err != hipSuccess) {
     (void)hipStreamSynchronize(s);  // the staging buffer is reused by the next call
     return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   }
-  SideStream* side = H.split2 ? side_stream() : nullptr;
-  if (H.split2 && !side) {
+  SideStream* side = H.split2 || spec_probe >= 2 ? side_stream() : nullptr;
+  if ((H.split2 || spec_probe >= 2) && !side) {
     (void)hipStreamSynchronize(s);
     return set_error(DN_ERR_HIP, "%s: side stream", name);
   }
-  uint64_t off = 0, coff = 0;
-  for (int k = 0; k < 3; ++k) {
-    const Level& l = lv[k];
-    if (!l.jobs.empty()) {
-      const char* jpr = tune_env("DN_MT_JUMP_PROBE");
-      const JumpArgs ja{dwin, djobs + off, static_cast<uint32_t>(l.jobs.size()),
-                        jpr ? static_cast<uint32_t>(std::atoi(jpr)) : 0u, rt_dev};
-      const dim3 grid(static_cast<uint32_t>(l.jobs.size() / static_cast<size_t>(l.W)));
-      if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, s, ja);
-      else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, s, ja);
+  auto launch_levels = [&](hipStream_t ls, uint32_t* wins) {
+    uint64_t off = 0, coff = 0;
+    for (int k = 0; k < 3; ++k) {
+      const Level& l = lv[k];
+      if (!l.jobs.empty()) {
+        const char* jpr = tune_env("DN_MT_JUMP_PROBE");
+        const JumpArgs ja{wins, djobs + off, static_cast<uint32_t>(l.jobs.size()),
+                          jpr ? static_cast<uint32_t>(std::atoi(jpr)) : 0u, rt_dev};
+        const dim3 grid(static_cast<uint32_t>(l.jobs.size() / static_cast<size_t>(l.W)));
+        if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, ls, ja);
+        else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, ls, ja);
+      }
+      if (!l.comb.empty())
+        hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(l.comb.size())), dim3(640), 0, ls, wins,
+                           dcomb + coff);
+      off += l.jobs.size();
+      coff += l.comb.size();
+      // split2: the first half's windows are complete after level 0
+      if (H.split2 && k == 0) err = hipEventRecord(side->levels, ls);
     }
-    if (!l.comb.empty())
-      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(l.comb.size())), dim3(640), 0, s, dwin,
-                         dcomb + coff);
-    off += l.jobs.size();
-    coff += l.comb.size();
-    // split2: the first half's windows are complete after level 0
-    if (side && k == 0) err = hipEventRecord(side->levels, s);
+  };
+  auto probe_levels = [&]() {
+    if (!side->buf || side->buf_bytes < scratch_bytes) {
+      if (side->buf) (void)hipFree(side->buf);
+      side->buf = nullptr;
+      side->buf_bytes = 0;
+      if (hipMalloc(&side->buf, scratch_bytes) != hipSuccess) return hipErrorOutOfMemory;
+      side->buf_bytes = scratch_bytes;
+    }
+    hipError_t e = hipStreamWaitEvent(side->s, side->copy, 0);
+    launch_levels(side->s, reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(side->buf) + kHead) + kMtN);
+    if (e == hipSuccess) e = hipEventRecord(side->spec, side->s);
+    side->pending = true;
+    return e;
+  };
+  if (spec_probe == 0) {
+    if (!hit) launch_levels(s, dwin);  // (a hit's windows are in place)
+  } else if (spec_probe >= 2) {
+    err = hipEventRecord(side->copy, s);
+    if (err == hipSuccess && side->pending) err = hipStreamWaitEvent(s, side->spec, 0);
+    if (err == hipSuccess && spec_probe == 2) err = probe_levels();
   }
   GenArgs ga{};
   ga.wins = dwin;
@@ -1737,7 +1938,17 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   ga.back = static_cast<uint32_t>(H.back);
   const char* pr = tune_env("DN_MT_PROBE");
   ga.probe = pr ? static_cast<uint32_t>(std::atoi(pr)) : 0u;
-  if (side) {
+  if (tail_fin) {
+    // the last substream's frame: position 0 = stream position idx + (S - 1) L
+    const uint64_t base = static_cast<uint64_t>(idx) + (S - 1) * (17 * mt_sub_draws(ki));
+    ga.tail_fin = 1u;
+    ga.fin_lo = static_cast<int32_t>(static_cast<int64_t>(ftf) - static_cast<int64_t>(base));
+    ga.next_lo = static_cast<int32_t>(static_cast<int64_t>(idx + words) - static_cast<int64_t>(base));
+  }
+  const uint32_t nwg = static_cast<uint32_t>(S) + (tail_fin ? 0u : 1u);  // + the final-state wave
+  ga.sub_n = nwg;
+  bool side_used = false;  // work of this call on the speculation side stream
+  if (H.split2) {
     // substreams [0, S/2) on the side stream once level 0 is done (beside
     // level 1's jumps), then [S/2, S] and the final-state wave on the call's
     // stream after level 1; the call's stream then waits for the side stream
@@ -1749,19 +1960,39 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     launch_gen(g1, side->s);
     if (err == hipSuccess) err = hipEventRecord(side->gen, side->s);
     ga.sub_lo = half;
-    ga.sub_n = static_cast<uint32_t>(S) + 1u - half;
+    ga.sub_n = nwg - half;
     launch_gen(ga, s);
     if (err == hipSuccess) err = hipStreamWaitEvent(s, side->gen, 0);
+  } else if (spec_next) {
+    // the generation, whose last substream also writes the next call's W_idx
+    // into row -1 of the other buffer; then on the side stream the next
+    // call's jump levels from it, while this call's host side finishes and
+    // the next call's begins
+    uint8_t* nb = static_cast<uint8_t*>(sp->buf[spec_dst]);
+    ga.next_win = reinterpret_cast<uint32_t*>(nb + kHead);
+    launch_gen(ga, s);
+    err = hipEventRecord(sp->win, s);
+    if (err == hipSuccess) err = hipStreamWaitEvent(sp->side, sp->win, 0);
+    side_used = true;
+    launch_levels(sp->side, reinterpret_cast<uint32_t*>(nb + kHead) + kMtN);
+    if (err == hipSuccess) err = hipEventRecord(sp->done, sp->side);
+    ++sp->launched;
   } else {
     launch_gen(ga, s);
+    if (err == hipSuccess && spec_probe == 3) err = probe_levels();
   }
-  if (err != hipSuccess) {
+  // an early exit waits for this call's side work too (it writes the staging buffer)
+  auto drain = [&]() {
     (void)hipStreamSynchronize(s);
+    if (side_used) (void)hipStreamSynchronize(sp->side);
+  };
+  if (err != hipSuccess) {
+    drain();
     return set_error(DN_ERR_HIP, "%s: side stream: %s", name, hipGetErrorString(err));
   }
   err = hipGetLastError();
   if (err != hipSuccess) {
-    (void)hipStreamSynchronize(s);
+    drain();
     return set_error(DN_ERR_HIP, "%s: launch: %s", name, hipGetErrorString(err));
   }
 
@@ -1770,13 +2001,27 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
 #endif
   const hipError_t serr = mt_wait(s);
   if (err == hipSuccess) err = serr;
-  if (err != hipSuccess) return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
+  if (err != hipSuccess) {
+    if (side_used) (void)hipStreamSynchronize(sp->side);
+    return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
+  }
+  if (hit) ++sp->hits;
   // DN_MT_FORCE_RETRY=1 (tuning build) takes the rejected-draw exit so the
   // caller's host fallback can be exercised.
   const char* fr = tune_env("DN_MT_FORCE_RETRY");
   if (head[0] || (fr && fr[0] == '1')) return set_error(DN_ERR_RETRY, "%s: a draw was rejected; redo on the host", name);
   if (sig >= 0) std::memcpy(mt_state, head + 256 / 4, kMtN * 4);
   *mt_index = fidx;
+  if (sp) {
+    // where this call ended; the next call, if it starts here, uses the
+    // speculated windows (spec_next) or speculates itself
+    sp->have_end = true;
+    sp->ncoef = ncoef;
+    sp->idx = fidx;
+    std::memcpy(sp->state, mt_state, kMtN * 4);
+    sp->armed = spec_next;
+    if (spec_next) sp->next = spec_dst;
+  }
   return DN_OK;
 }
 
@@ -1882,4 +2127,22 @@ extern "C" int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, co
                          else if (threshold == 3) launch_gen<3>(ga, s);
                          else launch_gen<5>(ga, s);
                        });
+}
+
+// The current device's speculation counters (DN_MT_SPEC): out[0] calls that
+// used speculated windows, out[1] speculations a call did not match, out[2]
+// speculations launched, out[3] 1 if one is armed now (the device's state is
+// made here if no draw has made it yet: all zero).
+extern "C" int dn_mt19937_spec_stats(uint64_t* out) {
+  if (!out) return set_error(DN_ERR_ARG, "dn_mt19937_spec_stats: null pointer");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(DN_ERR_HIP, "dn_mt19937_spec_stats: no device");
+  SpecState* sp = spec_slot(dev);
+  if (!sp) return set_error(DN_ERR_HIP, "dn_mt19937_spec_stats: speculation state");
+  std::lock_guard<std::mutex> g(sp->m);
+  out[0] = sp->hits;
+  out[1] = sp->misses;
+  out[2] = sp->launched;
+  out[3] = sp->armed ? 1u : 0u;
+  return DN_OK;
 }

@@ -48,7 +48,7 @@ EXPORTS = (
     "dn_mt19937_split_device", "dn_mt19937_split_supported", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
     "dn_shamir_eval_at_host", "dn_block_granularity", "dn_block_alloc", "dn_block_free", "dn_block_probe_rows",
     "dn_block_record", "dn_block_ready", "dn_block_acquire", "dn_block_retired_bytes",
-    "dn_mt19937_rt_rows_embedded",
+    "dn_mt19937_rt_rows_embedded", "dn_mt19937_spec_stats",
 )
 
 
@@ -169,6 +169,9 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_block_acquire.argtypes = [vp, vp, i32]
     L.dn_mt19937_rt_rows_embedded.restype = i32
     L.dn_mt19937_rt_rows_embedded.argtypes = []
+    if hasattr(L, "dn_mt19937_spec_stats"):  # (an A/B baseline built from an older revision may lack it)
+        L.dn_mt19937_spec_stats.restype = i32
+        L.dn_mt19937_spec_stats.argtypes = [ctypes.POINTER(u64)]
     L.dn_block_retired_bytes.restype = i32
     L.dn_block_retired_bytes.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.dn_block_probe_rows.restype = i32
@@ -508,6 +511,14 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
     if not ip:
         _mt_set_state(rng, version, gauss, state, index)
     return True
+
+
+def mt_spec_stats() -> dict:
+    """The current device's draw speculation counters (dn_mt19937_spec_stats):
+    hits, misses, launched, armed."""
+    out = (ctypes.c_uint64 * 4)()
+    check(lib().dn_mt19937_spec_stats(out))
+    return {"hits": int(out[0]), "misses": int(out[1]), "launched": int(out[2]), "armed": bool(out[3])}
 
 
 # ------------------------------------------------------------------ host (byte API)

@@ -203,6 +203,14 @@ int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_
  * differences (use the draw and the split); DN_ERR_RETRY as above (the shares
  * are then incomplete: redo the draw on the host and split).
  * Replaces per element: shamir.py:55-66 (make_shares) with :59-61's draws.
+ *
+ * Both device draws speculate on a loop of equal draws (DN_MT_SPEC, on by
+ * default): from the second of two calls of one size a call also computes,
+ * on a library-owned side stream and buffer, the jump windows of a next draw
+ * of the same size starting where this one ends, and a next call whose size,
+ * index and 624-word array match uses them instead of jumping (no visible
+ * difference but time; any mismatch is a miss).  The side work holds two
+ * library-owned buffers of dn_mt19937_device_scratch_bytes per device.
  */
 int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, const int64_t* secrets, void* shares,
                             uint64_t n_elem, int threshold, int n_shares, void* scratch, uint64_t scratch_bytes,
@@ -317,6 +325,14 @@ int dn_mt19937_skip(uint32_t* mt_state, int32_t* mt_index, uint64_t words);
  * rows would be computed at run time instead.
  */
 int dn_mt19937_rt_rows_embedded(void);
+
+/*
+ * The current device's draw speculation counters: out[0] calls that used
+ * speculated windows, out[1] speculations the next call did not match,
+ * out[2] speculations launched, out[3] 1 while one is armed.  (Diagnostics for
+ * tests and the bench; no reference counterpart.)
+ */
+int dn_mt19937_spec_stats(uint64_t* out);
 
 /*
  * Share wire codec over whole vectors (shamir.py:28-45 `_share_to_bytes` /
