@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "delta-node_amd"))
 import torch  # noqa: E402
 
 from delta_node.crypto import shamir  # noqa: E402
-from delta_node.crypto.shamir import _native, field  # noqa: E402
+from delta_node.crypto.shamir import _native, field, memory  # noqa: E402
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
@@ -72,6 +72,20 @@ for lg in [int(x) for x in os.environ.get("SIZES", "12,16,20,22,23,24").split(",
         if r:
             ts.append((time.perf_counter() - t0) * 1e3)
     res[f"2^{lg}_lone_ms"] = min(ts)
+    if lg >= 20:  # lone calls into a pooled share block (the placement make_shares_vec allocates)
+        pb = memory.share_block((5, field.vec_bytes(n)), dev)
+        ts = []
+        for r in range(6):
+            f = shamir.SecretShare(3)
+            f.random.seed(2000 + r)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            f.make_shares_vec(x, 5, out=pb)
+            torch.cuda.synchronize()
+            if r:
+                ts.append((time.perf_counter() - t0) * 1e3)
+        res[f"2^{lg}_lone_pooled_ms"] = min(ts)
+        del pb
     del out, want, co
 res["equal_draw_then_split"] = ok
 try:
