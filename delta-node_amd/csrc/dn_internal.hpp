@@ -60,6 +60,9 @@ const uint64_t* mt_direct_rows_l14(uint64_t S, uint64_t* version);
 // generator of the embedded table, csrc/gen_mt_rt_rows.cpp); false: no
 // carry-less multiply, or a row disagreed with the tabulated ones.
 bool mt_rt_rows_compute(uint64_t* out, uint64_t nrows);
+// out[kMtPolyWords] = x^e mod P (the jump polynomial of e words); false: no
+// carry-less multiply on this host
+bool mt_xpow_mod(uint64_t e, uint64_t* out);
 // The generator's checksum of the embedded table (two words written after it).
 void mt_rt_rows_checksum(const uint64_t* words, uint64_t n, uint64_t out[2]);
 }  // namespace dn

@@ -184,6 +184,34 @@ void mt_rt_rows_checksum(const uint64_t* w, uint64_t n, uint64_t out[2]) {
   out[1] = c;
 }
 
+// x^e mod P by square-and-multiply (Barrett squarings; a multiply by x is a
+// shift and at most one XOR of P): the jump polynomial of e words, for the
+// speculated next call's W_idx (mt19937_device.hip, DN_MT_SPEC beside the
+// generation).  ~30 products: a few ms, once per draw size.
+bool mt_xpow_mod(uint64_t e, uint64_t* out) {
+  if (!__builtin_cpu_supports("pclmul")) return false;
+  static Barrett* br = new Barrett;  // (never destroyed; built once: ~20 ms)
+  std::vector<uint64_t> r(kW, 0), t(kW);
+  r[0] = 1;
+  for (int b = e ? 63 - __builtin_clzll(e) : -1; b >= 0; --b) {
+    br->mulmod(r.data(), r.data(), t.data());
+    r.swap(t);
+    if ((e >> b) & 1u) {
+      uint64_t carry = 0;
+      for (int k = 0; k < kW; ++k) {
+        const uint64_t w = r[k];
+        r[k] = (w << 1) | carry;
+        carry = w >> 63;
+      }
+      if (bit(r.data(), kDeg)) {
+        for (int k = 0; k < kW; ++k) r[k] ^= kP[0][k];
+      }
+    }
+  }
+  std::memcpy(out, r.data(), sizeof(uint64_t) * kW);
+  return true;
+}
+
 bool mt_rt_rows_compute(uint64_t* out, uint64_t nrows) {
   if (!__builtin_cpu_supports("pclmul") || nrows == 0) return false;
   Barrett br;

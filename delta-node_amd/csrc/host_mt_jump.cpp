@@ -165,3 +165,11 @@ extern "C" int dn_mt19937_skip(uint32_t* mt_state, int32_t* mt_index, uint64_t w
   *mt_index = fidx;
   return DN_OK;
 }
+
+// x^words mod P (host_gf2poly.cpp's mt_xpow_mod): dn_shamir.h
+extern "C" int dn_mt19937_jump_poly(uint64_t words, uint64_t* out) {
+  if (!out) return dn::set_error(DN_ERR_ARG, "dn_mt19937_jump_poly: null pointer");
+  if (!dn::mt_xpow_mod(words, out))
+    return dn::set_error(DN_ERR_UNSUPPORTED, "dn_mt19937_jump_poly: no carry-less multiply");
+  return DN_OK;
+}

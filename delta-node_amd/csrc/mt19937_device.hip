@@ -430,6 +430,143 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   }
 }
 
+// ---- the two-bit jump: a workgroup small enough to sit beside the generation
+// mt_jump_kernel's Horner over 2-bit chunks of g (32 per word of g): the
+// table holds T[v] = sum over bits j of v of f^j(W) for v = 0..3, each as
+// the 704 consecutive stream positions q = 64 k + m (T-stream word q - 16;
+// zero outside 0..685) — 11 KB of LDS instead of 83 — so a workgroup fits on
+// a CU beside the generation's eight 17.7 KB rings (160 KB).  Chunk t of a
+// step reads, for window register r = 1..10, position 64 (r - 1) + lane + 62
+// - 2 t of T[c_t]: ten ds_read_b32 from one address (immediate offsets 256 B
+// apart, 64 consecutive words per instruction: conflict-free), two chunks
+// XORed per v_bitop3 as in mt_jump_kernel — twice its table bytes and XORs
+// per word of g.  For the speculated levels that run beside the generation
+// (DN_MT_SPEC_BESIDE).
+constexpr int kE2Val = 704;                                        // words per table value
+constexpr int kE2Words = 4 * kE2Val;                               // 2816 words, 11 KB
+static_assert(kE2Words >= 1024 + kMtN + 63, "the stepping ring and the source stream fit in the table's space");
+
+__device__ __forceinline__ void table_words2(const uint32_t* E, uint32_t c, int t, uint32_t lane, uint32_t (&x)[10]) {
+  const uint32_t* p = E + c * static_cast<uint32_t>(kE2Val) + lane + static_cast<uint32_t>(62 - 2 * t);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) x[i] = p[64 * i];
+}
+
+template <int K>
+__device__ __forceinline__ void jump_mega2(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E, uint32_t lane,
+                                           uint64_t gw) {
+  uint32_t x[2][2][10];
+  append64<K>(Q, L);
+  table_words2(E, static_cast<uint32_t>(gw >> 62) & 3u, 0, lane, x[0][0]);
+  table_words2(E, static_cast<uint32_t>(gw >> 60) & 3u, 1, lane, x[0][1]);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    if (p < 15) {
+      table_words2(E, static_cast<uint32_t>(gw >> (58 - 4 * p)) & 3u, 2 * p + 2, lane, x[(p + 1) & 1][0]);
+      table_words2(E, static_cast<uint32_t>(gw >> (56 - 4 * p)) & 3u, 2 * p + 3, lane, x[(p + 1) & 1][1]);
+    }
+#pragma unroll
+    for (int r = 1; r < 11; ++r)
+      Q[(r + K) % 11] = xor3(Q[(r + K) % 11], x[p & 1][0][r - 1], x[p & 1][1][r - 1]);
+  }
+}
+
+template <int... ks>
+__device__ __forceinline__ void jump_run2(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E, uint32_t lane,
+                                          const uint64_t* g, int wi, int top, std::integer_sequence<int, ks...>) {
+  const_u64_t* gc = (const_u64_t*)(g);
+  const int tu = __builtin_amdgcn_readfirstlane(top);
+  uint64_t gws[sizeof...(ks)];
+  ((void)(gws[ks] = gc[__builtin_amdgcn_readfirstlane(wi - ks <= tu ? wi - ks : tu)]), ...);  // in range
+  ((void)(gws[ks] = (wi - ks) <= tu ? gws[ks] : 0ull), ...);
+  ((void)jump_mega2<ks>(Q, L, E, lane, gws[ks]), ...);
+}
+
+// Jobs as mt_jump_kernel's (W jumps or parts of one source and lo per
+// workgroup); the source stream is staged in the table's space and read into
+// registers before the table overwrites it.
+template <int W>
+__global__ void __launch_bounds__(64 * W) mt_jump2_kernel(const JumpArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t E[kE2Words];
+  uint32_t* ext = E + 1024;  // words 0 .. 686 of the source stream, until the table is built
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  const uint32_t j0 = blockIdx.x * W;
+  const JumpJob* jp = a.jobs + __builtin_amdgcn_readfirstlane(j0 + wid < a.njobs ? j0 + wid : j0);
+  const int32_t poly = __builtin_amdgcn_readfirstlane(jp->poly), dsti = __builtin_amdgcn_readfirstlane(jp->dst);
+  const int32_t lo = __builtin_amdgcn_readfirstlane(a.jobs[j0].span) & 0xffff;
+  const int32_t hi = __builtin_amdgcn_readfirstlane(jp->span) >> 16;
+  const uint32_t* src = a.wins + static_cast<int64_t>(__builtin_amdgcn_readfirstlane(a.jobs[j0].src)) * kMtN;
+  if (lo == 0) {
+    for (uint32_t i = tid; i < kMtN; i += 64u * W) ext[i] = src[i];
+    __syncthreads();
+    if (tid < 63u) ext[kMtN + tid] = mt_mix(ext[tid], ext[tid + 1], ext[tid + kMtM]);
+    __syncthreads();
+  } else {
+    // words 64 lo .. 64 lo + 686 of the stream, stepped in a 1024-word ring (E[0, 1024))
+    uint32_t* ring = E;
+    for (uint32_t i = tid; i < kMtN; i += 64u * W) ring[i] = src[i];
+    __syncthreads();
+    const uint32_t need = 64u * static_cast<uint32_t>(lo) + 687u;
+    for (uint32_t base = 0; base + kMtN < need; base += kMtN - kMtM) {
+      for (uint32_t tt = tid; tt < static_cast<uint32_t>(kMtN - kMtM); tt += 64u * W) {
+        const uint32_t i = base + tt;
+        ring[(i + kMtN) & 1023u] = mt_mix(ring[i & 1023u], ring[(i + 1u) & 1023u], ring[(i + kMtM) & 1023u]);
+      }
+      __syncthreads();
+    }
+    for (uint32_t i = tid; i < 687u; i += 64u * W) ext[i] = ring[(64u * static_cast<uint32_t>(lo) + i) & 1023u];
+    __syncthreads();
+  }
+  // the table: position q holds T[v] word q - 16 = (v & 1 ? s_j : 0) ^ (v & 2 ? s_{j+1} : 0)
+  constexpr int kQ = (kE2Val + 64 * W - 1) / (64 * W);
+  uint32_t w0[kQ], w1[kQ];
+#pragma unroll
+  for (int k = 0; k < kQ; ++k) {
+    const int q = static_cast<int>(tid) + 64 * W * k, j = q - 16;
+    const bool in = q < kE2Val && j >= 0 && j < 686;
+    w0[k] = in ? ext[j] : 0u;
+    w1[k] = in ? ext[j + 1] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kQ; ++k) {
+    const int q = static_cast<int>(tid) + 64 * W * k;
+    if (q < kE2Val) {
+      E[q] = 0u;
+      E[kE2Val + q] = w0[k];
+      E[2 * kE2Val + q] = w1[k];
+      E[3 * kE2Val + q] = w0[k] ^ w1[k];
+    }
+  }
+  __syncthreads();
+  if (j0 + wid >= a.njobs || dsti < 0) return;
+
+  const uint64_t* g = poly < kMtDirectBase ? &kMtPolysDev[0][0][0] + static_cast<uint64_t>(poly) * kMtPolyWords
+                      : poly < kMtRtBase
+                          ? &kMtDirectDev[0][0][0] + static_cast<uint64_t>(poly - kMtDirectBase) * kMtPolyWords
+                          : a.rt + static_cast<uint64_t>(poly - kMtRtBase) * kMtPolyWords;
+  uint32_t Q[11];
+#pragma unroll
+  for (int r = 0; r < 11; ++r) Q[r] = 0u;
+  Lanes L;
+  L.pa = static_cast<int>(((lane + 16u) & 63u) * 4u);
+  L.pb = static_cast<int>(((lane + 17u) & 63u) * 4u);
+  L.pm = static_cast<int>(((lane + 29u) & 63u) * 4u);
+  L.la = lane < 16u, L.lb = lane < 17u, L.lm = lane < 29u;
+  int top = hi - 1;
+  while (top > lo && g[top] == 0ull) --top;
+  top = __builtin_amdgcn_readfirstlane(top);
+  if (a.probe != 1u)
+    for (int wi = lo + 11 * ((top - lo) / 11) + 10; wi >= lo + 10; wi -= 11)
+      jump_run2(Q, L, E, lane, g, wi, top, std::make_integer_sequence<int, 11>{});
+  uint32_t* dst = a.wins + static_cast<int64_t>(dsti) * kMtN;
+#pragma unroll
+  for (int r = 0; r < 11; ++r) {
+    const int i = 64 * r + static_cast<int>(lane) - 16;
+    if (i >= 0 && i < kMtN) dst[i] = Q[r];
+  }
+}
+
 // The parts of a split level XORed into their jumps' windows: one thread per
 // window word, the (at most 16) part loads issued together.
 __global__ void __launch_bounds__(640) mt_combine_kernel(uint32_t* wins, const CombineJob* cj) {
@@ -441,7 +578,7 @@ __global__ void __launch_bounds__(640) mt_combine_kernel(uint32_t* wins, const C
 #pragma unroll
   for (int32_t j = 0; j < kMaxParts; ++j)
     if (j < c.parts) x ^= p[static_cast<uint64_t>(j) * kMtN];
-  wins[static_cast<uint64_t>(c.dst) * kMtN + i] = x;
+  wins[static_cast<int64_t>(c.dst) * kMtN + i] = x;  // (dst -1: the W_idx row)
 }
 
 // ------------------------------------------------------------------ generation
@@ -1264,7 +1401,7 @@ std::vector<int32_t> part_cuts(int P, int W) {
 }
 
 void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::pair<int32_t, int32_t>>>>& srcs,
-                int32_t prow0, int p_force = 0) {
+                int32_t prow0, int p_force = 0, int w_force = 0) {
   size_t n = 0, most = 0;  // jumps, and the most of one source
   for (auto& sp : srcs) n += sp.second.size(), most = std::max(most, sp.second.size());
   if (n == 0) return;
@@ -1273,8 +1410,9 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
   // DN_MT_PARTS_B (tuning build): the part count of levels of 256 jumps or more
   const char* pb = n >= 256 ? tune_env("DN_MT_PARTS_B") : nullptr;
   if (pb && std::atoi(pb) >= 1) P = std::min(kMaxParts, std::atoi(pb));
-  const size_t per = std::min<size_t>(kJumpWaves, std::max<size_t>(2, (n * P + 255) / 256));
+  size_t per = std::min<size_t>(kJumpWaves, std::max<size_t>(2, (n * P + 255) / 256));
   L.W = std::min(per, most) > 8 ? 16 : 8;
+  if (w_force > 0) L.W = w_force, per = static_cast<size_t>(w_force);  // (mt_jump2_kernel's workgroups)
   if (P == 1) {
     for (auto& sp : srcs) push_groups(L, sp.first, sp.second, per);
     return;
@@ -1394,7 +1532,10 @@ struct MtHost {
   bool rt = false;  // one direct level through the runtime rows
   bool split2 = false;  // that level in two halves (DN_MT_SPLIT2)
   Level lv[3];
-  std::vector<uint32_t> jobs;  // the levels' jobs, then their combine jobs, as copied to the device
+  Level beside;  // rt: the direct level for mt_jump2_kernel<4> (whole jumps, 4 per workgroup)
+  Level j0;      // rt: one jump, row S -> row -1 by x^(17 ncoef) (the rt pointer), in parts, mt_jump2_kernel<4>
+  std::vector<uint32_t> jobs;  // the levels' jobs, their combine jobs, beside's jobs, j0's jobs and combine job
+  uint64_t beside_off = 0, j0_off = 0, j0_comb_off = 0;  // word offsets in `jobs`
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
 };
 thread_local MtHost tls_mt;
@@ -1426,8 +1567,22 @@ MtHost& mt_levels(uint64_t S, int ki) {
   if (H.S != S || H.ki != ki || H.back != back || H.parts_b != parts_b || H.rt != rt || H.split2 != split2) {
     for (auto& l : H.lv) l = Level();
     build_levels(S, ki, back, rt, H.lv, split2);
+    H.beside = Level();
+    if (rt && !split2) {
+      std::vector<std::pair<int32_t, int32_t>> pd;
+      for (uint64_t s = 1; s < S; ++s)
+        if (mt_window_needed(static_cast<uint32_t>(s), S, back))
+          pd.push_back({kMtRtBase + static_cast<int32_t>(s - 1), static_cast<int32_t>(s)});
+      push_level(H.beside, {{-1, pd}}, static_cast<int32_t>(S + 1), 1, 4);
+      H.j0 = Level();
+      push_level(H.j0, {{static_cast<int32_t>(S), {{kMtRtBase, -1}}}}, static_cast<int32_t>(S + 1), kMaxParts, 4);
+    } else {
+      H.j0 = Level();
+    }
     uint64_t nj = 0, nc = 0;
     for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
+    nj += H.beside.jobs.size() + H.j0.jobs.size();
+    nc += H.j0.comb.size();
     H.part_rows = 0;
     for (auto& l : H.lv)
       for (auto& c : l.comb) H.part_rows = std::max<uint64_t>(H.part_rows, c.first + c.parts - (S + 1));
@@ -1441,6 +1596,14 @@ MtHost& mt_levels(uint64_t S, int ki) {
       std::memcpy(H.jobs.data() + o, l.comb.data(), l.comb.size() * sizeof(CombineJob));
       o += l.comb.size() * sizeof(CombineJob) / 4;
     }
+    H.beside_off = o;
+    std::memcpy(H.jobs.data() + o, H.beside.jobs.data(), H.beside.jobs.size() * sizeof(JumpJob));
+    o += H.beside.jobs.size() * sizeof(JumpJob) / 4;
+    H.j0_off = o;
+    std::memcpy(H.jobs.data() + o, H.j0.jobs.data(), H.j0.jobs.size() * sizeof(JumpJob));
+    o += H.j0.jobs.size() * sizeof(JumpJob) / 4;
+    H.j0_comb_off = o;
+    std::memcpy(H.jobs.data() + o, H.j0.comb.data(), H.j0.comb.size() * sizeof(CombineJob));
     H.S = S;
     H.ki = ki;
     H.back = back;
@@ -1659,14 +1822,22 @@ SideStream* side_stream() {
 #ifndef DN_MT_TAIL_FIN
 #define DN_MT_TAIL_FIN 1
 #endif
+// The speculated levels of a runtime-direct-level draw (2^24 scale) beside
+// the generation rather than after it (mt_jump2_kernel<4>; tuning build:
+// DN_MT_SPEC_BESIDE=0 off)
+#ifndef DN_MT_SPEC_BESIDE
+#define DN_MT_SPEC_BESIDE 1
+#endif
 // draws of fewer coefficients than this do not speculate (tuning build: DN_MT_SPEC_MIN)
 #ifndef DN_MT_SPEC_MIN
 #define DN_MT_SPEC_MIN (1ull << 23)
 #endif
 struct SpecState {
   std::mutex m;
-  hipStream_t side = nullptr;
-  hipEvent_t win = nullptr, done = nullptr;  // the next call's W_idx written (call stream), its levels done
+  hipStream_t side = nullptr, side2 = nullptr;
+  hipEvent_t win = nullptr, done = nullptr;  // this call's windows in place (call stream), the side streams done
+  hipEvent_t j0ev = nullptr, done2 = nullptr;
+  bool widx2 = false;  // beside: buf[next ^ 1]'s row -1 holds the W_idx of the call after the armed one
   void* buf[2] = {nullptr, nullptr};
   uint64_t bytes = 0;  // of each buffer
   bool armed = false;  // buf[next] holds (at `done`) the windows of a call starting as below
@@ -1676,6 +1847,9 @@ struct SpecState {
   uint32_t state[kMtN];
   bool have_end = false;  // ncoef, idx, state: where the previous call ended
   uint64_t hits = 0, misses = 0, launched = 0;
+  uint64_t* xpow = nullptr;  // device: x^xpow_words mod P (the next call's W_idx from this one's)
+  uint64_t xpow_words = 0;
+  bool xpow_failed = false;  // no carry-less multiply here, or the upload failed: no beside levels
 };
 
 std::mutex& spec_table_mutex() {
@@ -1689,6 +1863,9 @@ SpecState* spec_slot(int dev) {  // created once per device, never destroyed (th
   if (!table[dev]) {
     auto* x = new SpecState;
     if (hipStreamCreateWithFlags(&x->side, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&x->side2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&x->j0ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->done2, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&x->win, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess)
       return nullptr;  // (leaks the half-made state: a runtime that cannot make a stream has bigger problems)
@@ -1697,11 +1874,34 @@ SpecState* spec_slot(int dev) {  // created once per device, never destroyed (th
   return table[dev];
 }
 
+// x^words mod P on the device for the beside chain's first jump (computed on
+// the host once per draw size: ~30 Barrett products, a few ms)
+bool spec_xpow(SpecState& sp, uint64_t words) {
+  if (sp.xpow_failed) return false;
+  if (sp.xpow && sp.xpow_words == words) return true;
+  std::vector<uint64_t> g(kMtPolyWords);
+  if (!mt_xpow_mod(words, g.data()) ||
+      (!sp.xpow && hipMalloc(reinterpret_cast<void**>(&sp.xpow), kMtPolyWords * sizeof(uint64_t)) != hipSuccess)) {
+    sp.xpow_failed = true;
+    return false;
+  }
+  (void)hipStreamSynchronize(sp.side);  // the previous size's polynomial may still be read
+  (void)hipStreamSynchronize(sp.side2);
+  if (hipMemcpy(sp.xpow, g.data(), kMtPolyWords * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) {
+    sp.xpow_failed = true;
+    return false;
+  }
+  sp.xpow_words = words;
+  return true;
+}
+
 // both buffers at least `need` bytes (false: allocation failed; no speculation)
 bool spec_buffers(SpecState& sp, uint64_t need) {
   if (sp.bytes >= need && sp.buf[0] && sp.buf[1]) return true;
-  (void)hipStreamSynchronize(sp.side);  // nothing of ours uses them once the side stream is idle
+  (void)hipStreamSynchronize(sp.side);  // nothing of ours uses them once the side streams are idle
+  (void)hipStreamSynchronize(sp.side2);
   sp.armed = false;
+  sp.widx2 = false;
   for (void*& b : sp.buf)
     if (b) (void)hipFree(b), b = nullptr;
   sp.bytes = 0;
@@ -1813,7 +2013,9 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   // 2 = skipped, and the same levels run on the side stream into a buffer of
   // their own, launched before the generation and awaited by the next call's
   // generation — the cost of a next call's speculative levels beside this
-  // call's generation; 3 = as 2, launched after the generation.
+  // call's generation; 3 = as 2, launched after the generation; 4 = as 2 with
+  // the runtime direct level by mt_jump2_kernel<4> (beside the generation);
+  // 5 = the call's own levels by mt_jump2_kernel<4> (its time alone).
   const char* spp = tune_env("DN_MT_SPEC_PROBE");
   const int spec_probe = spp ? std::atoi(spp) : 0;
   // the speculation state (DN_MT_SPEC): this call's draw may have been
@@ -1835,7 +2037,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
       if (!spl.owns_lock()) sp = nullptr;
     }
   }
-  bool hit = false, spec_next = false;
+  bool hit = false, spec_next = false, widx2 = false;
   if (sp) {
     // this call continues the previous one (same size, starting where it
     // ended): a hit if that call speculated, and a reason to speculate again
@@ -1843,12 +2045,22 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
                       !std::memcmp(sp->state, mt_state, kMtN * 4);
     hit = cont && sp->armed;
     if (sp->armed && !hit) ++sp->misses;
+    widx2 = hit && sp->widx2;
     sp->armed = false;
+    sp->widx2 = false;
     sp->have_end = false;
     spec_next = cont && spec_buffers(*sp, dn_mt19937_device_scratch_bytes(n_elem, tm1));
   }
+  // beside (DN_MT_SPEC_BESIDE, runtime direct level only): the next call's
+  // W_idx by one jump from this call's, then its level, both by
+  // mt_jump2_kernel<4> on the side stream beside this call's generation
+  const char* sbe = tune_env("DN_MT_SPEC_BESIDE");
+  const bool beside = spec_next && (sbe ? sbe[0] != '0' : DN_MT_SPEC_BESIDE != 0) && !H.beside.jobs.empty() &&
+                      !H.j0.jobs.empty() && spec_xpow(*sp, words);
   const int spec_dst = sp ? sp->next ^ 1 : 0;  // the buffer the next call's windows go to
-  uint8_t* sc = hit ? static_cast<uint8_t*>(sp->buf[sp->next]) : static_cast<uint8_t*>(scratch);
+  // a hit generates from its speculated buffer; a beside call runs in the
+  // other library buffer too (the side stream reads its W_idx from there)
+  uint8_t* sc = hit || beside ? static_cast<uint8_t*>(sp->buf[sp->next]) : static_cast<uint8_t*>(scratch);
   const JumpJob* djobs = static_cast<const JumpJob*>(jobs_dev);
   const CombineJob* dcomb = reinterpret_cast<const CombineJob*>(djobs + njobs);
   uint32_t* dwin = reinterpret_cast<uint32_t*>(sc + kHead) + kMtN;  // row 0
@@ -1857,6 +2069,8 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   // if it is still running)
   hipError_t err = (spec_next || hit) && hipEventQuery(sp->done) != hipSuccess ? hipStreamWaitEvent(s, sp->done, 0)
                                                                               : hipSuccess;
+  if (err == hipSuccess && (spec_next || hit) && hipEventQuery(sp->done2) != hipSuccess)
+    err = hipStreamWaitEvent(s, sp->done2, 0);
   if (err == hipSuccess) err = hipMemcpyAsync(sc, pin, wpre * 4, hipMemcpyHostToDevice, s);
   if (err != hipSuccess) {
     (void)hipStreamSynchronize(s);  // the staging buffer is reused by the next call
@@ -1888,6 +2102,13 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
       if (H.split2 && k == 0) err = hipEventRecord(side->levels, ls);
     }
   };
+  auto probe_beside = [&](hipStream_t ls, uint32_t* wins) {  // DN_MT_SPEC_PROBE=4: the rt level by mt_jump2_kernel<4>
+    const Level& l = H.beside;
+    if (l.jobs.empty()) return;
+    const JumpJob* bj = reinterpret_cast<const JumpJob*>(static_cast<const uint32_t*>(jobs_dev) + H.beside_off);
+    const JumpArgs ja{wins, bj, static_cast<uint32_t>(l.jobs.size()), 0u, rt_dev};
+    hipLaunchKernelGGL(mt_jump2_kernel<4>, dim3(static_cast<uint32_t>(l.jobs.size() / 4)), dim3(256), 0, ls, ja);
+  };
   auto probe_levels = [&]() {
     if (!side->buf || side->buf_bytes < scratch_bytes) {
       if (side->buf) (void)hipFree(side->buf);
@@ -1897,17 +2118,21 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
       side->buf_bytes = scratch_bytes;
     }
     hipError_t e = hipStreamWaitEvent(side->s, side->copy, 0);
-    launch_levels(side->s, reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(side->buf) + kHead) + kMtN);
+    uint32_t* pw = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(side->buf) + kHead) + kMtN;
+    if (spec_probe == 4) probe_beside(side->s, pw);
+    else launch_levels(side->s, pw);
     if (e == hipSuccess) e = hipEventRecord(side->spec, side->s);
     side->pending = true;
     return e;
   };
-  if (spec_probe == 0) {
+  if (spec_probe == 5) {
+    probe_beside(s, dwin);
+  } else if (spec_probe == 0) {
     if (!hit) launch_levels(s, dwin);  // (a hit's windows are in place)
   } else if (spec_probe >= 2) {
     err = hipEventRecord(side->copy, s);
     if (err == hipSuccess && side->pending) err = hipStreamWaitEvent(s, side->spec, 0);
-    if (err == hipSuccess && spec_probe == 2) err = probe_levels();
+    if (err == hipSuccess && (spec_probe == 2 || spec_probe == 4)) err = probe_levels();
   }
   GenArgs ga{};
   ga.wins = dwin;
@@ -1963,6 +2188,47 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     ga.sub_n = nwg - half;
     launch_gen(ga, s);
     if (err == hipSuccess) err = hipStreamWaitEvent(s, side->gen, 0);
+  } else if (beside) {
+    // Once this call's windows are in place, in workgroups of 11 KB that fit
+    // on a CU beside the generation's rings: on the side stream the next
+    // call's level into the other buffer from its W_idx (row -1 there) — which
+    // the previous call computed (widx2) or, first, one jump by x^(17 ncoef)
+    // from this call's W_idx computes (copied to row S, 32 parts + combine);
+    // on the second side stream the W_idx of the call after that, jumped from
+    // the next call's into this call's buffer (rows S, part rows and -1: none
+    // of them read by this call's generation).
+    uint8_t* nb = static_cast<uint8_t*>(sp->buf[spec_dst]);
+    uint32_t* nw = reinterpret_cast<uint32_t*>(nb + kHead) + kMtN;  // the next call's row 0
+    const uint32_t* hj = static_cast<const uint32_t*>(jobs_dev);
+    auto jump0 = [&](hipStream_t ls, uint32_t* w) {  // row S -> row -1 of w by x^(17 ncoef)
+      const JumpArgs j0{w, reinterpret_cast<const JumpJob*>(hj + H.j0_off), static_cast<uint32_t>(H.j0.jobs.size()), 0u,
+                        sp->xpow};
+      hipLaunchKernelGGL(mt_jump2_kernel<4>, dim3(static_cast<uint32_t>(H.j0.jobs.size() / 4)), dim3(256), 0, ls, j0);
+      hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(H.j0.comb.size())), dim3(640), 0, ls, w,
+                         reinterpret_cast<const CombineJob*>(hj + H.j0_comb_off));
+    };
+    err = hipEventRecord(sp->win, s);
+    launch_gen(ga, s);
+    side_used = true;
+    if (err == hipSuccess) err = hipStreamWaitEvent(sp->side, sp->win, 0);
+    if (err == hipSuccess) err = hipStreamWaitEvent(sp->side2, sp->win, 0);
+    if (!widx2) {
+      if (err == hipSuccess)
+        err = hipMemcpyAsync(nw + S * kMtN, dwin - kMtN, kMtN * 4, hipMemcpyDeviceToDevice, sp->side);
+      jump0(sp->side, nw);
+      if (err == hipSuccess) err = hipEventRecord(sp->j0ev, sp->side);
+      if (err == hipSuccess) err = hipStreamWaitEvent(sp->side2, sp->j0ev, 0);
+    }
+    const JumpArgs bl{nw, reinterpret_cast<const JumpJob*>(hj + H.beside_off), static_cast<uint32_t>(H.beside.jobs.size()),
+                      0u, rt_dev};
+    hipLaunchKernelGGL(mt_jump2_kernel<4>, dim3(static_cast<uint32_t>(H.beside.jobs.size() / 4)), dim3(256), 0, sp->side,
+                       bl);
+    if (err == hipSuccess) err = hipEventRecord(sp->done, sp->side);
+    if (err == hipSuccess)
+      err = hipMemcpyAsync(dwin + S * kMtN, nw - kMtN, kMtN * 4, hipMemcpyDeviceToDevice, sp->side2);
+    jump0(sp->side2, dwin);
+    if (err == hipSuccess) err = hipEventRecord(sp->done2, sp->side2);
+    ++sp->launched;
   } else if (spec_next) {
     // the generation, whose last substream also writes the next call's W_idx
     // into row -1 of the other buffer; then on the side stream the next
@@ -1984,7 +2250,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   // an early exit waits for this call's side work too (it writes the staging buffer)
   auto drain = [&]() {
     (void)hipStreamSynchronize(s);
-    if (side_used) (void)hipStreamSynchronize(sp->side);
+    if (side_used) (void)hipStreamSynchronize(sp->side), (void)hipStreamSynchronize(sp->side2);
   };
   if (err != hipSuccess) {
     drain();
@@ -2002,7 +2268,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   const hipError_t serr = mt_wait(s);
   if (err == hipSuccess) err = serr;
   if (err != hipSuccess) {
-    if (side_used) (void)hipStreamSynchronize(sp->side);
+    if (side_used) (void)hipStreamSynchronize(sp->side), (void)hipStreamSynchronize(sp->side2);
     return set_error(DN_ERR_HIP, "%s: %s", name, hipGetErrorString(err));
   }
   if (hit) ++sp->hits;
@@ -2020,6 +2286,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     sp->idx = fidx;
     std::memcpy(sp->state, mt_state, kMtN * 4);
     sp->armed = spec_next;
+    sp->widx2 = beside;  // this call's buffer now holds the W_idx after the next call's
     if (spec_next) sp->next = spec_dst;
   }
   return DN_OK;

@@ -48,7 +48,7 @@ EXPORTS = (
     "dn_mt19937_split_device", "dn_mt19937_split_supported", "dn_shamir_make_shares_host", "dn_shamir_resolve_shares_host",
     "dn_shamir_eval_at_host", "dn_block_granularity", "dn_block_alloc", "dn_block_free", "dn_block_probe_rows",
     "dn_block_record", "dn_block_ready", "dn_block_acquire", "dn_block_retired_bytes",
-    "dn_mt19937_rt_rows_embedded", "dn_mt19937_spec_stats",
+    "dn_mt19937_rt_rows_embedded", "dn_mt19937_spec_stats", "dn_mt19937_jump_poly",
 )
 
 
@@ -169,9 +169,12 @@ def _load(path: str) -> ctypes.CDLL:
     L.dn_block_acquire.argtypes = [vp, vp, i32]
     L.dn_mt19937_rt_rows_embedded.restype = i32
     L.dn_mt19937_rt_rows_embedded.argtypes = []
-    if hasattr(L, "dn_mt19937_spec_stats"):  # (an A/B baseline built from an older revision may lack it)
+    if hasattr(L, "dn_mt19937_spec_stats"):  # (an A/B baseline built from an older revision may lack these)
         L.dn_mt19937_spec_stats.restype = i32
         L.dn_mt19937_spec_stats.argtypes = [ctypes.POINTER(u64)]
+    if hasattr(L, "dn_mt19937_jump_poly"):
+        L.dn_mt19937_jump_poly.restype = i32
+        L.dn_mt19937_jump_poly.argtypes = [u64, ctypes.POINTER(u64)]
     L.dn_block_retired_bytes.restype = i32
     L.dn_block_retired_bytes.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
     L.dn_block_probe_rows.restype = i32
@@ -511,6 +514,15 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
     if not ip:
         _mt_set_state(rng, version, gauss, state, index)
     return True
+
+
+def mt_jump_poly(words: int):
+    """x^words mod P as 312 little-endian uint64 words (dn_mt19937_jump_poly)."""
+    import numpy as np
+
+    out = (ctypes.c_uint64 * 312)()
+    check(lib().dn_mt19937_jump_poly(words, out))
+    return np.frombuffer(out, dtype=np.uint64).copy()
 
 
 def mt_spec_stats() -> dict:

@@ -335,6 +335,16 @@ int dn_mt19937_rt_rows_embedded(void);
 int dn_mt19937_spec_stats(uint64_t* out);
 
 /*
+ * The MT19937 jump polynomial of `words` words: out[312] = x^words mod P (P
+ * the characteristic polynomial of the one-word transition; the window after
+ * `words` words is out(f) applied to the window).  The speculated next draw's
+ * start window is jumped to by it.  DN_ERR_UNSUPPORTED on a host without
+ * carry-less multiply.  (No reference counterpart: random.Random advances word
+ * by word.)
+ */
+int dn_mt19937_jump_poly(uint64_t words, uint64_t* out);
+
+/*
  * Share wire codec over whole vectors (shamir.py:28-45 `_share_to_bytes` /
  * `_bytes_to_share`, serialize/hex.py:44-50).  Record e of the packed stream
  * is exactly the reference's bytes for share (x, y_e):

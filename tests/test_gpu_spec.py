@@ -251,3 +251,31 @@ def test_final_state_by_the_last_substream(n, tm1, pre, tail, monkeypatch):
         assert _native.mt_draw_coeffs_device(b, n, tm1, got)
     assert torch.equal(got, want)
     assert a.getstate() == b.getstate()
+
+
+@pytest.mark.parametrize("n,tm1,pre", [(1 << 23, 2, 0), ((1 << 24) + 1, 1, 333), ((1 << 22) + 1000, 4, 7)])
+def test_two_bit_jump_kernel_equals_host_draw(n, tm1, pre, monkeypatch):
+    """mt_jump2_kernel (2-bit chunks, an 11 KB table, four waves per
+    workgroup: the kernel that fits beside the generation) computing the
+    2^24-scale draw's direct level in place of mt_jump_kernel (tuning build,
+    DN_MT_SPEC_PROBE=5): the host draw's block and final state."""
+    a = random.Random(n + tm1 + pre)
+    a.getrandbits(32 * pre)
+    b = random.Random()
+    b.setstate(a.getstate())
+    want = torch.from_numpy(_native.mt_draw_coeffs(a, n, tm1)).to(dev())
+    got = torch.zeros((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    monkeypatch.setenv("DN_MT_SPEC_PROBE", "5")
+    with _native.library(_native.TUNING_LIB):
+        assert _native.mt_draw_coeffs_device(b, n, tm1, got)
+    assert torch.equal(got, want)
+    assert a.getstate() == b.getstate()
+
+
+def test_loop_without_beside_levels(monkeypatch):
+    """The 2^24-scale speculation with the beside chain off (tuning build,
+    DN_MT_SPEC_BESIDE=0: the next call's W_idx from the last substream, its
+    level after the generation): hits, and the host draw's shares and state."""
+    monkeypatch.setenv("DN_MT_SPEC_BESIDE", "0")
+    with _native.library(_native.TUNING_LIB):
+        _loop_case((1 << 23) + 9, 3, 5, 100)

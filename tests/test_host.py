@@ -45,6 +45,36 @@ def test_library_exports_header_symbols():
     assert sorted(_native.EXPORTS + _mask_native.EXPORTS + codec.EXPORTS + mimc7.EXPORTS + aes.EXPORTS) == syms
 
 
+def _mt_step_window(w: np.ndarray, n: int) -> np.ndarray:
+    """The 624-word MT window advanced n words (word 624 + i = mix(i, i + 1, i + 397))."""
+    s = [int(x) for x in w]
+    for i in range(n):
+        y = (s[i] & 0x80000000) | (s[i + 1] & 0x7FFFFFFF)
+        s.append(s[i + 397] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0))
+    return np.array(s[n:n + 624], dtype=np.uint32)
+
+
+@pytest.mark.parametrize("words", [1, 700, 5000, 17 * 16384 - 624])
+def test_jump_polynomial_advances_the_window(words):
+    """dn_mt19937_jump_poly(words) = x^words mod P: applied to a window by
+    Horner (r <- f(r) ^ g_i W from the top coefficient down, f = one word of
+    the transition) it gives the window stepped `words` words — the jump the
+    speculated next draw starts from (DN_MT_SPEC beside the generation)."""
+    g = _native.mt_jump_poly(words)
+    bits = np.unpackbits(g.view(np.uint8), bitorder="little")[:19937]
+    rng = np.random.default_rng(words)
+    w = rng.integers(0, 1 << 32, 624, dtype=np.uint64).astype(np.uint32)
+    top = int(np.nonzero(bits)[0].max())
+    r = [0] * 624
+    wl = [int(x) for x in w]
+    for i in range(top, -1, -1):
+        y = (r[0] & 0x80000000) | (r[1] & 0x7FFFFFFF)
+        r = r[1:] + [r[397] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)]
+        if bits[i]:
+            r = [a ^ b for a, b in zip(r, wl)]
+    assert np.array_equal(np.array(r, dtype=np.uint32), _mt_step_window(w, words))
+
+
 def test_embedded_mt_jump_rows_pass_their_checks():
     """The build-time table of 2048 direct jump rows (csrc/gen_mt_rt_rows.cpp,
     embedded by csrc/mt_rt_rows14.S) carries its generator's checksum and
