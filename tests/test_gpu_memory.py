@@ -166,10 +166,14 @@ def _ref_shares(seed, sec, t, n):
     return out
 
 
-def test_share_block_not_reused_while_another_stream_still_reads_it():
+def test_share_block_not_reused_while_another_stream_still_reads_it(monkeypatch):
     """The returned shares belong to the caller (shamir.py:62-66): a block
     freed while stream A still has work queued on it is not handed to a
-    request on stream B — A's queued read sees A's shares, B gets its own."""
+    request on stream B — A's queued read sees A's shares, B gets its own.
+    (Blocks unprobed here: a probe that rejects a block frees it, and the
+    free may wait for the device, i.e. for A's queued work — the race this
+    test needs would be lost on a box where the first try is rejected.)"""
+    monkeypatch.setattr(memory, "PROBE_MIN_BYTES", 1 << 62)
     memory.empty_cache()
     N = 1 << 18
     sec_a = torch.randint(-(1 << 62), 1 << 62, (N,), dtype=torch.int64, device=dev())
