@@ -430,40 +430,51 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
   }
 }
 
-// ---- the two-bit jump: a workgroup small enough to sit beside the generation
-// mt_jump_kernel's Horner over 2-bit chunks of g (32 per word of g): the
-// table holds T[v] = sum over bits j of v of f^j(W) for v = 0..3, each as
-// the 704 consecutive stream positions q = 64 k + m (T-stream word q - 16;
-// zero outside 0..685) — 11 KB of LDS instead of 83 — so a workgroup fits on
-// a CU beside the generation's eight 17.7 KB rings (160 KB).  Chunk t of a
-// step reads, for window register r = 1..10, position 64 (r - 1) + lane + 62
-// - 2 t of T[c_t]: ten ds_read_b32 from one address (immediate offsets 256 B
-// apart, 64 consecutive words per instruction: conflict-free), two chunks
-// XORed per v_bitop3 as in mt_jump_kernel — twice its table bytes and XORs
-// per word of g.  For the speculated levels that run beside the generation
-// (DN_MT_SPEC_BESIDE).
-constexpr int kE2Val = 704;                                        // words per table value
-constexpr int kE2Words = 4 * kE2Val;                               // 2816 words, 11 KB
-static_assert(kE2Words >= 1024 + kMtN + 63, "the stepping ring and the source stream fit in the table's space");
+// ---- jumps with a contiguous table: the two-bit kernel that sits beside the
+// generation, and a four-bit variant
+// mt_jump_kernel's Horner over CB-bit chunks of g (64 / CB per word of g)
+// with the table T[v] = sum over bits j of v of f^j(W), v < 2^CB, stored as
+// the 704 consecutive stream positions q = 64 k + m of each value (T-stream
+// word q - 16; zero outside the used range): chunk t of a step reads, for
+// window register r = 1..10, position 64 (r - 1) + lane + 64 - CB - CB t of
+// T[c_t] — ten ds_read_b32 from one address (immediate offsets 256 B apart,
+// 64 consecutive words per instruction: conflict-free, no wrapped copy), two
+// chunks XORed per v_bitop3 as in mt_jump_kernel.
+//  * CB = 2, W = 4 (mt_jumpc_kernel<4, 2>): 4 values, 11 KB — a workgroup fits
+//    on a CU beside the generation's eight 17.7 KB rings (160 KB), at twice
+//    the table bytes and XORs per word of g; the speculated levels that run
+//    beside the generation (DN_MT_SPEC_BESIDE).
+//  * CB = 4 (DN_MT_JUMP4B, tuning build): 16 values, 45 KB instead of
+//    mt_jump_kernel's 83 (no wrapped copy), so two 16-wave workgroups share
+//    a CU (<= 64 VGPRs): twice the waves per CU at twice the LDS
+//    instructions (b32, same bytes) — an A/B of the direct level.
+constexpr int kE2Val = 704;  // words per table value
+template <int CB>
+constexpr int kECWords = (1 << CB) * kE2Val;  // 2816 words (11 KB) at CB = 2, 11264 (45 KB) at CB = 4
+static_assert(kECWords<2> >= 1024 + kMtN + 63, "the stepping ring and the source stream fit in the table's space");
 
-__device__ __forceinline__ void table_words2(const uint32_t* E, uint32_t c, int t, uint32_t lane, uint32_t (&x)[10]) {
-  const uint32_t* p = E + c * static_cast<uint32_t>(kE2Val) + lane + static_cast<uint32_t>(62 - 2 * t);
+template <int CB>
+__device__ __forceinline__ void table_words_c(const uint32_t* E, uint32_t c, int t, uint32_t lane, uint32_t (&x)[10]) {
+  const uint32_t* p = E + c * static_cast<uint32_t>(kE2Val) + lane + static_cast<uint32_t>(64 - CB - CB * t);
 #pragma unroll
   for (int i = 0; i < 10; ++i) x[i] = p[64 * i];
 }
 
-template <int K>
-__device__ __forceinline__ void jump_mega2(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E, uint32_t lane,
-                                           uint64_t gw) {
+template <int CB, int K>
+__device__ __forceinline__ void jump_mega_c(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E, uint32_t lane,
+                                            uint64_t gw) {
+  constexpr int NC = 64 / CB;  // chunks per word of g
+  constexpr uint32_t kMask = (1u << CB) - 1u;
+  auto cv = [&](int t) { return static_cast<uint32_t>(gw >> (64 - CB * (t + 1))) & kMask; };
   uint32_t x[2][2][10];
   append64<K>(Q, L);
-  table_words2(E, static_cast<uint32_t>(gw >> 62) & 3u, 0, lane, x[0][0]);
-  table_words2(E, static_cast<uint32_t>(gw >> 60) & 3u, 1, lane, x[0][1]);
+  table_words_c<CB>(E, cv(0), 0, lane, x[0][0]);
+  table_words_c<CB>(E, cv(1), 1, lane, x[0][1]);
 #pragma unroll
-  for (int p = 0; p < 16; ++p) {
-    if (p < 15) {
-      table_words2(E, static_cast<uint32_t>(gw >> (58 - 4 * p)) & 3u, 2 * p + 2, lane, x[(p + 1) & 1][0]);
-      table_words2(E, static_cast<uint32_t>(gw >> (56 - 4 * p)) & 3u, 2 * p + 3, lane, x[(p + 1) & 1][1]);
+  for (int p = 0; p < NC / 2; ++p) {
+    if (p < NC / 2 - 1) {
+      table_words_c<CB>(E, cv(2 * p + 2), 2 * p + 2, lane, x[(p + 1) & 1][0]);
+      table_words_c<CB>(E, cv(2 * p + 3), 2 * p + 3, lane, x[(p + 1) & 1][1]);
     }
 #pragma unroll
     for (int r = 1; r < 11; ++r)
@@ -471,23 +482,23 @@ __device__ __forceinline__ void jump_mega2(uint32_t (&Q)[11], const Lanes& L, co
   }
 }
 
-template <int... ks>
-__device__ __forceinline__ void jump_run2(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E, uint32_t lane,
-                                          const uint64_t* g, int wi, int top, std::integer_sequence<int, ks...>) {
+template <int CB, int... ks>
+__device__ __forceinline__ void jump_run_c(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E, uint32_t lane,
+                                           const uint64_t* g, int wi, int top, std::integer_sequence<int, ks...>) {
   const_u64_t* gc = (const_u64_t*)(g);
   const int tu = __builtin_amdgcn_readfirstlane(top);
   uint64_t gws[sizeof...(ks)];
   ((void)(gws[ks] = gc[__builtin_amdgcn_readfirstlane(wi - ks <= tu ? wi - ks : tu)]), ...);  // in range
   ((void)(gws[ks] = (wi - ks) <= tu ? gws[ks] : 0ull), ...);
-  ((void)jump_mega2<ks>(Q, L, E, lane, gws[ks]), ...);
+  ((void)jump_mega_c<CB, ks>(Q, L, E, lane, gws[ks]), ...);
 }
 
 // Jobs as mt_jump_kernel's (W jumps or parts of one source and lo per
 // workgroup); the source stream is staged in the table's space and read into
 // registers before the table overwrites it.
-template <int W>
-__global__ void __launch_bounds__(64 * W) mt_jump2_kernel(const JumpArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t E[kE2Words];
+template <int W, int CB>
+__global__ void __launch_bounds__(64 * W, CB == 4 ? 8 : 1) mt_jumpc_kernel(const JumpArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t E[kECWords<CB>];
   uint32_t* ext = E + 1024;  // words 0 .. 686 of the source stream, until the table is built
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
   const uint32_t j0 = blockIdx.x * W;
@@ -517,25 +528,28 @@ __global__ void __launch_bounds__(64 * W) mt_jump2_kernel(const JumpArgs a) {
     for (uint32_t i = tid; i < 687u; i += 64u * W) ext[i] = ring[(64u * static_cast<uint32_t>(lo) + i) & 1023u];
     __syncthreads();
   }
-  // the table: position q holds T[v] word q - 16 = (v & 1 ? s_j : 0) ^ (v & 2 ? s_{j+1} : 0)
+  // the table: position q holds T[v] word j = q - 16 = XOR of s_{j+b} over bits b of v
   constexpr int kQ = (kE2Val + 64 * W - 1) / (64 * W);
-  uint32_t w0[kQ], w1[kQ];
+  constexpr int kJEnd = 687 - (CB - 1);  // j + CB - 1 <= 686
+  uint32_t w[kQ][CB];
 #pragma unroll
   for (int k = 0; k < kQ; ++k) {
     const int q = static_cast<int>(tid) + 64 * W * k, j = q - 16;
-    const bool in = q < kE2Val && j >= 0 && j < 686;
-    w0[k] = in ? ext[j] : 0u;
-    w1[k] = in ? ext[j + 1] : 0u;
+    const bool in = q < kE2Val && j >= 0 && j < kJEnd;
+#pragma unroll
+    for (int b = 0; b < CB; ++b) w[k][b] = in ? ext[j + b] : 0u;
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kQ; ++k) {
     const int q = static_cast<int>(tid) + 64 * W * k;
     if (q < kE2Val) {
-      E[q] = 0u;
-      E[kE2Val + q] = w0[k];
-      E[2 * kE2Val + q] = w1[k];
-      E[3 * kE2Val + q] = w0[k] ^ w1[k];
+      uint32_t c[1 << CB];
+      c[0] = 0u;
+#pragma unroll
+      for (int v = 1; v < (1 << CB); ++v) c[v] = c[v & (v - 1)] ^ w[k][__builtin_ctz(v)];
+#pragma unroll
+      for (int v = 0; v < (1 << CB); ++v) E[v * kE2Val + q] = c[v];
     }
   }
   __syncthreads();
@@ -558,7 +572,7 @@ __global__ void __launch_bounds__(64 * W) mt_jump2_kernel(const JumpArgs a) {
   top = __builtin_amdgcn_readfirstlane(top);
   if (a.probe != 1u)
     for (int wi = lo + 11 * ((top - lo) / 11) + 10; wi >= lo + 10; wi -= 11)
-      jump_run2(Q, L, E, lane, g, wi, top, std::make_integer_sequence<int, 11>{});
+      jump_run_c<CB>(Q, L, E, lane, g, wi, top, std::make_integer_sequence<int, 11>{});
   uint32_t* dst = a.wins + static_cast<int64_t>(dsti) * kMtN;
 #pragma unroll
   for (int r = 0; r < 11; ++r) {
@@ -1412,7 +1426,7 @@ void push_level(Level& L, const std::vector<std::pair<int32_t, std::vector<std::
   if (pb && std::atoi(pb) >= 1) P = std::min(kMaxParts, std::atoi(pb));
   size_t per = std::min<size_t>(kJumpWaves, std::max<size_t>(2, (n * P + 255) / 256));
   L.W = std::min(per, most) > 8 ? 16 : 8;
-  if (w_force > 0) L.W = w_force, per = static_cast<size_t>(w_force);  // (mt_jump2_kernel's workgroups)
+  if (w_force > 0) L.W = w_force, per = static_cast<size_t>(w_force);  // (mt_jumpc_kernel's workgroups)
   if (P == 1) {
     for (auto& sp : srcs) push_groups(L, sp.first, sp.second, per);
     return;
@@ -1532,8 +1546,8 @@ struct MtHost {
   bool rt = false;  // one direct level through the runtime rows
   bool split2 = false;  // that level in two halves (DN_MT_SPLIT2)
   Level lv[3];
-  Level beside;  // rt: the direct level for mt_jump2_kernel<4> (whole jumps, 4 per workgroup)
-  Level j0;      // rt: one jump, row S -> row -1 by x^(17 ncoef) (the rt pointer), in parts, mt_jump2_kernel<4>
+  Level beside;  // rt: the direct level for mt_jumpc_kernel<4, 2> (whole jumps, 4 per workgroup)
+  Level j0;      // rt: one jump, row S -> row -1 by x^(17 ncoef) (the rt pointer), in parts, mt_jumpc_kernel<4, 2>
   std::vector<uint32_t> jobs;  // the levels' jobs, their combine jobs, beside's jobs, j0's jobs and combine job
   uint64_t beside_off = 0, j0_off = 0, j0_comb_off = 0;  // word offsets in `jobs`
   uint64_t part_rows = 0;      // part windows the largest split level writes (levels reuse them)
@@ -1823,7 +1837,7 @@ SideStream* side_stream() {
 #define DN_MT_TAIL_FIN 1
 #endif
 // The speculated levels of a runtime-direct-level draw (2^24 scale) beside
-// the generation rather than after it (mt_jump2_kernel<4>; tuning build:
+// the generation rather than after it (mt_jumpc_kernel<4, 2>; tuning build:
 // DN_MT_SPEC_BESIDE=0 off)
 #ifndef DN_MT_SPEC_BESIDE
 #define DN_MT_SPEC_BESIDE 1
@@ -2014,8 +2028,8 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   // their own, launched before the generation and awaited by the next call's
   // generation — the cost of a next call's speculative levels beside this
   // call's generation; 3 = as 2, launched after the generation; 4 = as 2 with
-  // the runtime direct level by mt_jump2_kernel<4> (beside the generation);
-  // 5 = the call's own levels by mt_jump2_kernel<4> (its time alone).
+  // the runtime direct level by mt_jumpc_kernel<4, 2> (beside the generation);
+  // 5 = the call's own levels by mt_jumpc_kernel<4, 2> (its time alone).
   const char* spp = tune_env("DN_MT_SPEC_PROBE");
   const int spec_probe = spp ? std::atoi(spp) : 0;
   // the speculation state (DN_MT_SPEC): this call's draw may have been
@@ -2053,7 +2067,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   }
   // beside (DN_MT_SPEC_BESIDE, runtime direct level only): the next call's
   // W_idx by one jump from this call's, then its level, both by
-  // mt_jump2_kernel<4> on the side stream beside this call's generation
+  // mt_jumpc_kernel<4, 2> on the side stream beside this call's generation
   const char* sbe = tune_env("DN_MT_SPEC_BESIDE");
   const bool beside = spec_next && (sbe ? sbe[0] != '0' : DN_MT_SPEC_BESIDE != 0) && !H.beside.jobs.empty() &&
                       !H.j0.jobs.empty() && spec_xpow(*sp, words);
@@ -2090,7 +2104,9 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
         const JumpArgs ja{wins, djobs + off, static_cast<uint32_t>(l.jobs.size()),
                           jpr ? static_cast<uint32_t>(std::atoi(jpr)) : 0u, rt_dev};
         const dim3 grid(static_cast<uint32_t>(l.jobs.size() / static_cast<size_t>(l.W)));
-        if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, ls, ja);
+        const char* j4 = tune_env("DN_MT_JUMP4B");  // tuning build: 16-wave levels by mt_jumpc_kernel<16, 4>
+        if (l.W == 16 && j4 && j4[0] == '1') hipLaunchKernelGGL((mt_jumpc_kernel<16, 4>), grid, dim3(64 * 16), 0, ls, ja);
+        else if (l.W == 16) hipLaunchKernelGGL(mt_jump_kernel<16>, grid, dim3(64 * 16), 0, ls, ja);
         else hipLaunchKernelGGL(mt_jump_kernel<8>, grid, dim3(64 * 8), 0, ls, ja);
       }
       if (!l.comb.empty())
@@ -2102,12 +2118,12 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
       if (H.split2 && k == 0) err = hipEventRecord(side->levels, ls);
     }
   };
-  auto probe_beside = [&](hipStream_t ls, uint32_t* wins) {  // DN_MT_SPEC_PROBE=4: the rt level by mt_jump2_kernel<4>
+  auto probe_beside = [&](hipStream_t ls, uint32_t* wins) {  // DN_MT_SPEC_PROBE=4: the rt level by mt_jumpc_kernel<4, 2>
     const Level& l = H.beside;
     if (l.jobs.empty()) return;
     const JumpJob* bj = reinterpret_cast<const JumpJob*>(static_cast<const uint32_t*>(jobs_dev) + H.beside_off);
     const JumpArgs ja{wins, bj, static_cast<uint32_t>(l.jobs.size()), 0u, rt_dev};
-    hipLaunchKernelGGL(mt_jump2_kernel<4>, dim3(static_cast<uint32_t>(l.jobs.size() / 4)), dim3(256), 0, ls, ja);
+    hipLaunchKernelGGL((mt_jumpc_kernel<4, 2>), dim3(static_cast<uint32_t>(l.jobs.size() / 4)), dim3(256), 0, ls, ja);
   };
   auto probe_levels = [&]() {
     if (!side->buf || side->buf_bytes < scratch_bytes) {
@@ -2203,7 +2219,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     auto jump0 = [&](hipStream_t ls, uint32_t* w) {  // row S -> row -1 of w by x^(17 ncoef)
       const JumpArgs j0{w, reinterpret_cast<const JumpJob*>(hj + H.j0_off), static_cast<uint32_t>(H.j0.jobs.size()), 0u,
                         sp->xpow};
-      hipLaunchKernelGGL(mt_jump2_kernel<4>, dim3(static_cast<uint32_t>(H.j0.jobs.size() / 4)), dim3(256), 0, ls, j0);
+      hipLaunchKernelGGL((mt_jumpc_kernel<4, 2>), dim3(static_cast<uint32_t>(H.j0.jobs.size() / 4)), dim3(256), 0, ls, j0);
       hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(H.j0.comb.size())), dim3(640), 0, ls, w,
                          reinterpret_cast<const CombineJob*>(hj + H.j0_comb_off));
     };
@@ -2221,7 +2237,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     }
     const JumpArgs bl{nw, reinterpret_cast<const JumpJob*>(hj + H.beside_off), static_cast<uint32_t>(H.beside.jobs.size()),
                       0u, rt_dev};
-    hipLaunchKernelGGL(mt_jump2_kernel<4>, dim3(static_cast<uint32_t>(H.beside.jobs.size() / 4)), dim3(256), 0, sp->side,
+    hipLaunchKernelGGL((mt_jumpc_kernel<4, 2>), dim3(static_cast<uint32_t>(H.beside.jobs.size() / 4)), dim3(256), 0, sp->side,
                        bl);
     if (err == hipSuccess) err = hipEventRecord(sp->done, sp->side);
     if (err == hipSuccess)

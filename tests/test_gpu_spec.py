@@ -279,3 +279,25 @@ def test_loop_without_beside_levels(monkeypatch):
     monkeypatch.setenv("DN_MT_SPEC_BESIDE", "0")
     with _native.library(_native.TUNING_LIB):
         _loop_case((1 << 23) + 9, 3, 5, 100)
+
+
+@pytest.mark.parametrize("parts", ["4", "8"])
+def test_four_bit_contiguous_jump_kernel_equals_host_draw(parts, monkeypatch):
+    """mt_jumpc_kernel<16, 4> (4-bit chunks, the 45 KB contiguous table, two
+    workgroups per CU) computing the 2^24-scale direct level in place of
+    mt_jump_kernel (tuning build: DN_MT_JUMP4B=1, DN_MT_PARTS_B parts per
+    jump): the host draw's block and final state."""
+    n, tm1 = (1 << 23) + 5, 2
+    a = random.Random(int(parts))
+    a.getrandbits(32 * 77)
+    b = random.Random()
+    b.setstate(a.getstate())
+    want = torch.from_numpy(_native.mt_draw_coeffs(a, n, tm1)).to(dev())
+    got = torch.zeros((tm1, field.vec_bytes(n)), dtype=torch.uint8, device=dev())
+    monkeypatch.setenv("DN_MT_JUMP4B", "1")
+    monkeypatch.setenv("DN_MT_PARTS_B", parts)
+    monkeypatch.setenv("DN_MT_SPEC", "0")
+    with _native.library(_native.TUNING_LIB):
+        assert _native.mt_draw_coeffs_device(b, n, tm1, got)
+    assert torch.equal(got, want)
+    assert a.getstate() == b.getstate()

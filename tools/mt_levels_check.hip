@@ -18,7 +18,8 @@
 namespace dn { int set_error(int c, const char*, ...) { return c; } int device_cu_count() { return 256; }
 uint64_t mt_jump_words() { return 0; } uint64_t mt_jump_max_subs() { return 262145; }
 void mt_advance_window(const uint32_t*, uint64_t, uint32_t*) {}
-const uint64_t* mt_direct_rows_l14(uint64_t, uint64_t*) { return nullptr; } }
+const uint64_t* mt_direct_rows_l14(uint64_t, uint64_t*) { return nullptr; }
+bool mt_xpow_mod(uint64_t, uint64_t*) { return false; } }
 using namespace dn;
 extern "C" uint64_t dn_m521_vec_bytes(uint64_t n) { return n; }
 int check(uint64_t S, int ki, int back, bool rt = false) {
