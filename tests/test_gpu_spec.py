@@ -301,3 +301,47 @@ def test_four_bit_contiguous_jump_kernel_equals_host_draw(parts, monkeypatch):
         assert _native.mt_draw_coeffs_device(b, n, tm1, got)
     assert torch.equal(got, want)
     assert a.getstate() == b.getstate()
+
+
+def test_speculation_under_threads_and_interleaved_objects():
+    """Two threads, each looping over the 2^24-scale draw with its own
+    SecretShare (the device's speculation state is taken by try_lock: a call
+    finding it busy runs unspeculated), then two objects interleaved on one
+    thread (each call misses the other's speculation): every call equals the
+    host draw + split, with the same final states."""
+    import threading
+
+    N = (1 << 23) + 3
+    sec = torch.from_numpy(secrets_int64(12, N)).to(dev())
+    res, err = {}, []
+
+    def run(i):
+        try:
+            torch.cuda.set_device(dev())
+            ss = shamir.SecretShare(3)
+            ss.random.seed(500 + i)
+            outs = [device_shares(ss, sec, N, 5) for _ in range(4)]
+            torch.cuda.synchronize()
+            res[i] = (outs, ss.random.getstate())
+        except Exception as e:  # surfaced below
+            err.append(e)
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not err, err
+    for i in range(2):
+        ref = shamir.SecretShare(3)
+        ref.random.seed(500 + i)
+        for got in res[i][0]:
+            assert torch.equal(got, host_shares(ref.random, sec, N, 3, 5))
+        assert ref.random.getstate() == res[i][1]
+    a, b, ra, rb = shamir.SecretShare(3), shamir.SecretShare(3), shamir.SecretShare(3), shamir.SecretShare(3)
+    for x, y in ((a, ra), (b, rb)):
+        x.random.seed(id(x) % 1000)
+        y.random.setstate(x.random.getstate())
+    for x, y in ((a, ra), (a, ra), (b, rb), (a, ra), (b, rb), (b, rb)):
+        assert torch.equal(device_shares(x, sec, N, 5), host_shares(y.random, sec, N, 3, 5))
+        assert x.random.getstate() == y.random.getstate()
