@@ -449,13 +449,31 @@ __global__ void __launch_bounds__(64 * W) mt_jump_kernel(const JumpArgs a) {
 //    a CU (<= 64 VGPRs): twice the waves per CU at twice the LDS
 //    instructions (b32, same bytes) — an A/B of the direct level.
 constexpr int kE2Val = 704;  // words per table value
+// CB = 3: 21 three-bit chunks and bit 0 alone (22 per word of g, offsets 61 - 3 t
+// and 0); T[0] = 0 is not stored (7 values, 19.3 KB: it still fits beside the
+// rings) — a zero chunk's read goes to T[1] and its XOR is skipped (the chunk
+// values are wave-uniform: a scalar branch per pair)
 template <int CB>
-constexpr int kECWords = (1 << CB) * kE2Val;  // 2816 words (11 KB) at CB = 2, 11264 (45 KB) at CB = 4
+constexpr int kNVal = CB == 3 ? 7 : (1 << CB);
+template <int CB>
+constexpr int kECWords = kNVal<CB> * kE2Val;  // 11 KB at CB = 2, 19.3 KB at 3, 45 KB at 4
+template <int CB>
+constexpr int kNChunks = CB == 3 ? 22 : 64 / CB;
 static_assert(kECWords<2> >= 1024 + kMtN + 63, "the stepping ring and the source stream fit in the table's space");
 
 template <int CB>
+__device__ __forceinline__ uint32_t chunk_val(uint64_t gw, int t) {
+  if constexpr (CB == 3) return t < 21 ? static_cast<uint32_t>(gw >> (61 - 3 * t)) & 7u : static_cast<uint32_t>(gw) & 1u;
+  else return static_cast<uint32_t>(gw >> (64 - CB * (t + 1))) & ((1u << CB) - 1u);
+}
+template <int CB>
+constexpr int chunk_off(int t) { return CB == 3 ? (t < 21 ? 61 - 3 * t : 0) : 64 - CB - CB * t; }
+template <int CB>
+__device__ __forceinline__ uint32_t chunk_row(uint32_t c) { return CB == 3 ? (c ? c - 1u : 0u) : c; }
+
+template <int CB>
 __device__ __forceinline__ void table_words_c(const uint32_t* E, uint32_t c, int t, uint32_t lane, uint32_t (&x)[10]) {
-  const uint32_t* p = E + c * static_cast<uint32_t>(kE2Val) + lane + static_cast<uint32_t>(64 - CB - CB * t);
+  const uint32_t* p = E + chunk_row<CB>(c) * static_cast<uint32_t>(kE2Val) + lane + static_cast<uint32_t>(chunk_off<CB>(t));
 #pragma unroll
   for (int i = 0; i < 10; ++i) x[i] = p[64 * i];
 }
@@ -463,22 +481,32 @@ __device__ __forceinline__ void table_words_c(const uint32_t* E, uint32_t c, int
 template <int CB, int K>
 __device__ __forceinline__ void jump_mega_c(uint32_t (&Q)[11], const Lanes& L, const uint32_t* E, uint32_t lane,
                                             uint64_t gw) {
-  constexpr int NC = 64 / CB;  // chunks per word of g
-  constexpr uint32_t kMask = (1u << CB) - 1u;
-  auto cv = [&](int t) { return static_cast<uint32_t>(gw >> (64 - CB * (t + 1))) & kMask; };
+  constexpr int NC = kNChunks<CB>;
   uint32_t x[2][2][10];
   append64<K>(Q, L);
-  table_words_c<CB>(E, cv(0), 0, lane, x[0][0]);
-  table_words_c<CB>(E, cv(1), 1, lane, x[0][1]);
+  table_words_c<CB>(E, chunk_val<CB>(gw, 0), 0, lane, x[0][0]);
+  table_words_c<CB>(E, chunk_val<CB>(gw, 1), 1, lane, x[0][1]);
 #pragma unroll
   for (int p = 0; p < NC / 2; ++p) {
     if (p < NC / 2 - 1) {
-      table_words_c<CB>(E, cv(2 * p + 2), 2 * p + 2, lane, x[(p + 1) & 1][0]);
-      table_words_c<CB>(E, cv(2 * p + 3), 2 * p + 3, lane, x[(p + 1) & 1][1]);
+      table_words_c<CB>(E, chunk_val<CB>(gw, 2 * p + 2), 2 * p + 2, lane, x[(p + 1) & 1][0]);
+      table_words_c<CB>(E, chunk_val<CB>(gw, 2 * p + 3), 2 * p + 3, lane, x[(p + 1) & 1][1]);
     }
+    if constexpr (CB == 3) {
+      const bool n0 = chunk_val<CB>(gw, 2 * p) != 0u, n1 = chunk_val<CB>(gw, 2 * p + 1) != 0u;
+      if (n0 && n1) {
 #pragma unroll
-    for (int r = 1; r < 11; ++r)
-      Q[(r + K) % 11] = xor3(Q[(r + K) % 11], x[p & 1][0][r - 1], x[p & 1][1][r - 1]);
+        for (int r = 1; r < 11; ++r)
+          Q[(r + K) % 11] = xor3(Q[(r + K) % 11], x[p & 1][0][r - 1], x[p & 1][1][r - 1]);
+      } else if (n0 || n1) {
+#pragma unroll
+        for (int r = 1; r < 11; ++r) Q[(r + K) % 11] ^= n0 ? x[p & 1][0][r - 1] : x[p & 1][1][r - 1];
+      }
+    } else {
+#pragma unroll
+      for (int r = 1; r < 11; ++r)
+        Q[(r + K) % 11] = xor3(Q[(r + K) % 11], x[p & 1][0][r - 1], x[p & 1][1][r - 1]);
+    }
   }
 }
 
@@ -549,7 +577,7 @@ __global__ void __launch_bounds__(64 * W, CB == 4 ? 8 : 1) mt_jumpc_kernel(const
 #pragma unroll
       for (int v = 1; v < (1 << CB); ++v) c[v] = c[v & (v - 1)] ^ w[k][__builtin_ctz(v)];
 #pragma unroll
-      for (int v = 0; v < (1 << CB); ++v) E[v * kE2Val + q] = c[v];
+      for (int v = CB == 3 ? 1 : 0; v < (1 << CB); ++v) E[(CB == 3 ? v - 1 : v) * kE2Val + q] = c[v];
     }
   }
   __syncthreads();
@@ -579,6 +607,20 @@ __global__ void __launch_bounds__(64 * W, CB == 4 ? 8 : 1) mt_jumpc_kernel(const
     const int i = 64 * r + static_cast<int>(lane) - 16;
     if (i >= 0 && i < kMtN) dst[i] = Q[r];
   }
+}
+
+// The chunk width of the kernel beside the generation (DN_MT_BESIDE_CB, 2 or
+// 3; tuning build: the env variable of that name)
+#ifndef DN_MT_BESIDE_CB
+#define DN_MT_BESIDE_CB 2
+#endif
+int beside_cb() {
+  const char* e = tune_env("DN_MT_BESIDE_CB");
+  return e ? (e[0] == '2' ? 2 : 3) : DN_MT_BESIDE_CB;
+}
+void launch_jumpc4(dim3 grid, hipStream_t s, const JumpArgs& ja) {
+  if (beside_cb() == 2) hipLaunchKernelGGL((mt_jumpc_kernel<4, 2>), grid, dim3(256), 0, s, ja);
+  else hipLaunchKernelGGL((mt_jumpc_kernel<4, 3>), grid, dim3(256), 0, s, ja);
 }
 
 // The parts of a split level XORed into their jumps' windows: one thread per
@@ -2123,7 +2165,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     if (l.jobs.empty()) return;
     const JumpJob* bj = reinterpret_cast<const JumpJob*>(static_cast<const uint32_t*>(jobs_dev) + H.beside_off);
     const JumpArgs ja{wins, bj, static_cast<uint32_t>(l.jobs.size()), 0u, rt_dev};
-    hipLaunchKernelGGL((mt_jumpc_kernel<4, 2>), dim3(static_cast<uint32_t>(l.jobs.size() / 4)), dim3(256), 0, ls, ja);
+    launch_jumpc4(dim3(static_cast<uint32_t>(l.jobs.size() / 4)), ls, ja);
   };
   auto probe_levels = [&]() {
     if (!side->buf || side->buf_bytes < scratch_bytes) {
@@ -2219,7 +2261,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     auto jump0 = [&](hipStream_t ls, uint32_t* w) {  // row S -> row -1 of w by x^(17 ncoef)
       const JumpArgs j0{w, reinterpret_cast<const JumpJob*>(hj + H.j0_off), static_cast<uint32_t>(H.j0.jobs.size()), 0u,
                         sp->xpow};
-      hipLaunchKernelGGL((mt_jumpc_kernel<4, 2>), dim3(static_cast<uint32_t>(H.j0.jobs.size() / 4)), dim3(256), 0, ls, j0);
+      launch_jumpc4(dim3(static_cast<uint32_t>(H.j0.jobs.size() / 4)), ls, j0);
       hipLaunchKernelGGL(mt_combine_kernel, dim3(static_cast<uint32_t>(H.j0.comb.size())), dim3(640), 0, ls, w,
                          reinterpret_cast<const CombineJob*>(hj + H.j0_comb_off));
     };
@@ -2237,8 +2279,7 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
     }
     const JumpArgs bl{nw, reinterpret_cast<const JumpJob*>(hj + H.beside_off), static_cast<uint32_t>(H.beside.jobs.size()),
                       0u, rt_dev};
-    hipLaunchKernelGGL((mt_jumpc_kernel<4, 2>), dim3(static_cast<uint32_t>(H.beside.jobs.size() / 4)), dim3(256), 0, sp->side,
-                       bl);
+    launch_jumpc4(dim3(static_cast<uint32_t>(H.beside.jobs.size() / 4)), sp->side, bl);
     if (err == hipSuccess) err = hipEventRecord(sp->done, sp->side);
     if (err == hipSuccess)
       err = hipMemcpyAsync(dwin + S * kMtN, nw - kMtN, kMtN * 4, hipMemcpyDeviceToDevice, sp->side2);

@@ -253,12 +253,15 @@ def test_final_state_by_the_last_substream(n, tm1, pre, tail, monkeypatch):
     assert a.getstate() == b.getstate()
 
 
+@pytest.mark.parametrize("cb", ["2", "3"])
 @pytest.mark.parametrize("n,tm1,pre", [(1 << 23, 2, 0), ((1 << 24) + 1, 1, 333), ((1 << 22) + 1000, 4, 7)])
-def test_two_bit_jump_kernel_equals_host_draw(n, tm1, pre, monkeypatch):
-    """mt_jump2_kernel (2-bit chunks, an 11 KB table, four waves per
-    workgroup: the kernel that fits beside the generation) computing the
+def test_two_bit_jump_kernel_equals_host_draw(n, tm1, pre, cb, monkeypatch):
+    """mt_jumpc_kernel<4, CB> (2-bit chunks in an 11 KB table, or 3-bit chunks
+    with bit 0 alone in a 19.3 KB table without T[0]; four waves per
+    workgroup: the kernels that fit beside the generation) computing the
     2^24-scale draw's direct level in place of mt_jump_kernel (tuning build,
-    DN_MT_SPEC_PROBE=5): the host draw's block and final state."""
+    DN_MT_SPEC_PROBE=5, DN_MT_BESIDE_CB): the host draw's block and final state."""
+    monkeypatch.setenv("DN_MT_BESIDE_CB", cb)
     a = random.Random(n + tm1 + pre)
     a.getrandbits(32 * pre)
     b = random.Random()
