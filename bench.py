@@ -1013,8 +1013,10 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
             "roofline_fused": roof("hbm", n * (8 + 5 * 66) / fm / 1e9,
                                    "8 B secret + 5 x 66 B shares per element (wall time of the whole call)"),
             "fused_ms_by_buffer": [x * 1e3 for x in fused_by_buf],
-            "timing": "wall time per call; fused_ms: the median over three output buffers of the best of "
-                      f"{reps} calls on each (after >= 0.15 s of warm-up calls)",
+            "timing": "wall time per call; fused_ms: lone calls (a fresh SecretShare each: nothing to speculate "
+                      f"on), the median over three output buffers of the best of {reps} calls on each (after >= "
+                      "0.15 s of warm-up calls); loop_ms_per_call: back-to-back calls on one SecretShare, where "
+                      "each call's jump level was speculated by the call before (DN_MT_SPEC)",
             "equal_draw_then_split_and_state": ok, "fused_ms_by_size": by_size,
             "loop_ms_per_call": loop}
 
