@@ -69,12 +69,16 @@
 #ifndef DN_AES_DEC_SPLIT
 #define DN_AES_DEC_SPLIT 2
 #endif
-// DN_AES_DEC_COAL (default 1): decode_kernel reads a wave's hex text line by
-// line and transposes it (as the encrypt kernel's text stores); 2 reads half
-// lines (hex_coalesce_half): slower, 1.98-2.01 vs 1.94-1.96 ms
-// (profiles/r05/s/).
+// DN_AES_DEC_COAL: the decrypt kernels read a wave's hex text line by line
+// and transpose it (as the encrypt kernel's text stores).  2 (default since
+// round 6): half lines, transposed by hex_coalesce_half (two permlane-swap
+// stages, no selects or DPP) — in the VALU-heavy one-pass decrypt
+// (decrypt_fused_kernel) 1.593-1.611 vs 1.615-1.646 ms, 4 of 4 alternating
+// pairs (profiles/r06/v/); the two-pass decode_kernel of round 5 was the
+// other way round (1.98-2.01 vs 1.94-1.96 ms, profiles/r05/s/).  1: whole
+// lines, three stages (hex_coalesce).
 #ifndef DN_AES_DEC_COAL
-#define DN_AES_DEC_COAL 1
+#define DN_AES_DEC_COAL 2
 #endif
 // DN_AES_NB (default 3): keystream blocks of an encrypt unit whose rounds run
 // interleaved (aes_blocks); 2 = two interleaved + one alone, 1 = one at a time.
