@@ -482,6 +482,9 @@ def mt_draw_coeffs_device(rng, n: int, tm1: int, out) -> bool:
     return True
 
 
+_MT_SPLIT_SHAPES: dict = {}  # (library, n, t, n_shares) -> (fused split supported, scratch bytes)
+
+
 def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool:
     """make_shares over n int64 secrets with coefficients drawn from `rng`
     (a random.Random) as n sequential make_shares calls would, draw and split
@@ -493,12 +496,20 @@ def mt_split_device(rng, secrets, shares, n: int, t: int, n_shares: int) -> bool
     if n == 0:
         return True
     L = lib()
-    if not L.dn_mt19937_split_supported(n, t, n_shares):
+    key = (id(L), n, t, n_shares)
+    shape = _MT_SPLIT_SHAPES.get(key)  # (supported, scratch bytes): two C calls per new shape only
+    if shape is None:
+        sup = bool(L.dn_mt19937_split_supported(n, t, n_shares))
+        shape = (sup, int(L.dn_mt19937_device_scratch_bytes(n, t - 1)) if sup else 0)
+        if len(_MT_SPLIT_SHAPES) >= 256:
+            _MT_SPLIT_SHAPES.clear()
+        _MT_SPLIT_SHAPES[key] = shape
+    if not shape[0]:
         return False  # before any allocation: the draw, then the split
     for name, x in (("secrets", secrets), ("shares", shares)):
         if not x.is_cuda or x.device != shares.device or not x.is_contiguous():
             raise ValueError(f"mt_split_device: {name} must be a contiguous tensor on the shares' HIP device")
-    sb = int(L.dn_mt19937_device_scratch_bytes(n, t - 1))
+    sb = shape[1]
     scratch = _mt_scratch(sb, shares.device)
     ip = _mt_inplace_addr(rng)  # the entry point writes the state only on success
     if ip:

@@ -443,8 +443,11 @@ def chunked_block(shape: Union[int, Sequence[int]], chunk_bytes: int = CHUNK_BYT
             if ptr is None:
                 raise
     blk = _Block(ptr, key, shape, pooled, stream)
-    with torch.cuda.device(dev.index):
+    if dev.index == torch.cuda.current_device():  # (a device switch costs two hipSetDevice per call)
         t = torch.as_tensor(blk, device=dev)
+    else:
+        with torch.cuda.device(dev.index):
+            t = torch.as_tensor(blk, device=dev)
     if t.data_ptr() != ptr or t.dtype != torch.uint8 or tuple(t.shape) != shape:
         raise RuntimeError("chunked_block: the tensor does not alias the block")
     _live[ptr] = weakref.ref(blk)
@@ -475,7 +478,7 @@ def share_block(shape: Union[int, Sequence[int]], device=None):
     nbytes = math.prod(shape)
     if nbytes < CHUNKED_MIN_BYTES:
         return torch.empty(shape, dtype=torch.uint8, device=dev)
-    if _retired() + nbytes > RETIRE_BUDGET and not _has_idle((dev.index, nbytes, CHUNK_BYTES)):
+    if not _has_idle((dev.index, nbytes, CHUNK_BYTES)) and _retired() + nbytes > RETIRE_BUDGET:
         _stats["va_fallbacks"] += 1  # address space retired past the budget: no new mappings
         return torch.empty(shape, dtype=torch.uint8, device=dev)
     return chunked_block(shape, CHUNK_BYTES, dev, probe=True)
