@@ -1624,17 +1624,19 @@ MtHost& mt_levels(uint64_t S, int ki) {
     for (auto& l : H.lv) l = Level();
     build_levels(S, ki, back, rt, H.lv, split2);
     H.beside = Level();
+    H.j0 = Level();
     if (rt && !split2) {
       std::vector<std::pair<int32_t, int32_t>> pd;
       for (uint64_t s = 1; s < S; ++s)
         if (mt_window_needed(static_cast<uint32_t>(s), S, back))
           pd.push_back({kMtRtBase + static_cast<int32_t>(s - 1), static_cast<int32_t>(s)});
       push_level(H.beside, {{-1, pd}}, static_cast<int32_t>(S + 1), 1, 4);
-      H.j0 = Level();
-      push_level(H.j0, {{static_cast<int32_t>(S), {{kMtRtBase, -1}}}}, static_cast<int32_t>(S + 1), kMaxParts, 4);
-    } else {
-      H.j0 = Level();
     }
+    // the next call's W_idx for a speculation beside the generation (any
+    // shape with jump levels: the levels of a small generation run beside it
+    // as they are, mt_device_run)
+    if (!split2 && S >= 2)
+      push_level(H.j0, {{static_cast<int32_t>(S), {{kMtRtBase, -1}}}}, static_cast<int32_t>(S + 1), kMaxParts, 4);
     uint64_t nj = 0, nc = 0;
     for (auto& l : H.lv) nj += l.jobs.size(), nc += l.comb.size();
     nj += H.beside.jobs.size() + H.j0.jobs.size();
@@ -1642,6 +1644,7 @@ MtHost& mt_levels(uint64_t S, int ki) {
     H.part_rows = 0;
     for (auto& l : H.lv)
       for (auto& c : l.comb) H.part_rows = std::max<uint64_t>(H.part_rows, c.first + c.parts - (S + 1));
+    for (auto& c : H.j0.comb) H.part_rows = std::max<uint64_t>(H.part_rows, c.first + c.parts - (S + 1));
     H.jobs.assign((nj * sizeof(JumpJob) + nc * sizeof(CombineJob)) / 4, 0u);
     uint64_t o = 0;
     for (auto& l : H.lv) {
@@ -1884,9 +1887,14 @@ SideStream* side_stream() {
 #ifndef DN_MT_SPEC_BESIDE
 #define DN_MT_SPEC_BESIDE 1
 #endif
-// draws of fewer coefficients than this do not speculate (tuning build: DN_MT_SPEC_MIN)
+// draws of fewer coefficients than this do not speculate after the
+// generation (tuning build: DN_MT_SPEC_MIN), nor beside it below
+// DN_MT_BESIDE_MIN (the levels of a small generation beside it, round 6)
 #ifndef DN_MT_SPEC_MIN
 #define DN_MT_SPEC_MIN (1ull << 23)
+#endif
+#ifndef DN_MT_BESIDE_MIN
+#define DN_MT_BESIDE_MIN (1ull << 16)
 #endif
 struct SpecState {
   std::mutex m;
@@ -2007,9 +2015,11 @@ namespace {
 // The device draw of n_elem * tm1 coefficients from CPython state
 // (mt_state, *mt_index): jump levels, then `launch_gen(ga, S)` (the
 // generation kernel: coefficients or fused split), then CPython's final state.
+constexpr uint64_t kCus = 256, kLdsPerCu = 160 * 1024;  // MI355X: CUs, LDS bytes per CU
+
 template <typename F>
 int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1, void* scratch,
-                  uint64_t scratch_bytes, void* stream, F launch_gen) {
+                  uint64_t scratch_bytes, void* stream, int ring_units, F launch_gen) {
   if (!mt_state || !mt_index) return set_error(DN_ERR_ARG, "%s: null pointer", name);
   if (tm1 < 0 || tm1 >= DN_MAX_THRESHOLD) return set_error(DN_ERR_ARG, "%s: t-1=%d", name, tm1);
   const int32_t idx = *mt_index;
@@ -2082,8 +2092,10 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   const bool tail_fin = sig >= 0 && (tfe ? tfe[0] != '0' : DN_MT_TAIL_FIN != 0);
   const char* spm = tune_env("DN_MT_SPEC_MIN");
   const uint64_t spec_min = spm ? std::strtoull(spm, nullptr, 10) : DN_MT_SPEC_MIN;
+  const char* bmn = tune_env("DN_MT_BESIDE_MIN");
+  const uint64_t beside_min = bmn ? std::strtoull(bmn, nullptr, 10) : DN_MT_BESIDE_MIN;
   const bool spec_on = (spe ? spe[0] != '0' : DN_MT_SPEC != 0) && spec_probe == 0 && !H.split2 && tail_fin &&
-                       njobs > 0 && ncoef >= spec_min;
+                       njobs > 0 && ncoef >= std::min(spec_min, beside_min);
   SpecState* sp = nullptr;
   std::unique_lock<std::mutex> spl;
   if (spec_on) {
@@ -2110,9 +2122,19 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
   // beside (DN_MT_SPEC_BESIDE, runtime direct level only): the next call's
   // W_idx by one jump from this call's, then its level, both by
   // mt_jumpc_kernel<4, 2> on the side stream beside this call's generation
+  // Other shapes: the levels as they are (mt_jump_kernel, 83 KB workgroups)
+  // when the generation's rings leave a CU that much LDS (a generation of at
+  // most ~1000 3-of-5 substreams: 2^22 coefficients and less), and when the
+  // generation outlasts them: substreams of 2^12 draws, or of 2^10 and at most
+  // 256 of them (loops of 2^20 / 2^16 elements -15 / -10 %; 512 substreams
+  // of 2^10 draws, 2^18 elements, +2.5 %: profiles/r06/y/).
   const char* sbe = tune_env("DN_MT_SPEC_BESIDE");
-  const bool beside = spec_next && (sbe ? sbe[0] != '0' : DN_MT_SPEC_BESIDE != 0) && !H.beside.jobs.empty() &&
+  const uint64_t gen_lds = (1u + 2u * 17u * 64u * static_cast<uint32_t>(ring_units) + 64u) * 4u;
+  const bool levels_fit = (S + kCus - 1) / kCus * gen_lds + (kEWords + kMtN + 64) * 4u <= kLdsPerCu;
+  const bool beside = spec_next && (sbe ? sbe[0] != '0' : DN_MT_SPEC_BESIDE != 0) && ncoef >= beside_min &&
+                      (H.rt ? !H.beside.jobs.empty() : levels_fit && (mt_sub_draws(ki) >= 4096 || S <= 256)) &&
                       !H.j0.jobs.empty() && spec_xpow(*sp, words);
+  if (!beside && ncoef < spec_min) spec_next = false;  // (no speculation after the generation this small)
   const int spec_dst = sp ? sp->next ^ 1 : 0;  // the buffer the next call's windows go to
   // a hit generates from its speculated buffer; a beside call runs in the
   // other library buffer too (the side stream reads its W_idx from there)
@@ -2277,9 +2299,13 @@ int mt_device_run(const char* name, uint32_t* mt_state, int32_t* mt_index, uint6
       if (err == hipSuccess) err = hipEventRecord(sp->j0ev, sp->side);
       if (err == hipSuccess) err = hipStreamWaitEvent(sp->side2, sp->j0ev, 0);
     }
-    const JumpArgs bl{nw, reinterpret_cast<const JumpJob*>(hj + H.beside_off), static_cast<uint32_t>(H.beside.jobs.size()),
-                      0u, rt_dev};
-    launch_jumpc4(dim3(static_cast<uint32_t>(H.beside.jobs.size() / 4)), sp->side, bl);
+    if (H.rt) {
+      const JumpArgs bl{nw, reinterpret_cast<const JumpJob*>(hj + H.beside_off),
+                        static_cast<uint32_t>(H.beside.jobs.size()), 0u, rt_dev};
+      launch_jumpc4(dim3(static_cast<uint32_t>(H.beside.jobs.size() / 4)), sp->side, bl);
+    } else {
+      launch_levels(sp->side, nw);
+    }
     if (err == hipSuccess) err = hipEventRecord(sp->done, sp->side);
     if (err == hipSuccess)
       err = hipMemcpyAsync(dwin + S * kMtN, nw - kMtN, kMtN * 4, hipMemcpyDeviceToDevice, sp->side2);
@@ -2415,7 +2441,7 @@ void launch_gen(GenArgs& ga, hipStream_t s) {
 extern "C" int dn_mt19937_draw_coeffs_device(uint32_t* mt_state, int32_t* mt_index, uint64_t n_elem, int tm1,
                                              void* coeffs, void* scratch, uint64_t scratch_bytes, void* stream) {
   if (n_elem && tm1 > 0 && !coeffs) return set_error(DN_ERR_ARG, "dn_mt19937_draw_coeffs_device: null pointer");
-  return mt_device_run("dn_mt19937_draw_coeffs_device", mt_state, mt_index, n_elem, tm1, scratch, scratch_bytes, stream,
+  return mt_device_run("dn_mt19937_draw_coeffs_device", mt_state, mt_index, n_elem, tm1, scratch, scratch_bytes, stream, 1,
                        [&](GenArgs& ga, hipStream_t s) {
                          ga.coeffs = static_cast<uint8_t*>(coeffs);
                          launch_gen<0>(ga, s);
@@ -2442,7 +2468,7 @@ extern "C" int dn_mt19937_split_device(uint32_t* mt_state, int32_t* mt_index, co
     return set_error(DN_ERR_UNSUPPORTED, "%s: fused form needs t in {2, 3, 5} and forward differences (t=%d, n=%d)",
                      name, threshold, n_shares);
   if (n_elem && (!secrets || !shares)) return set_error(DN_ERR_ARG, "%s: null pointer", name);
-  return mt_device_run(name, mt_state, mt_index, n_elem, threshold - 1, scratch, scratch_bytes, stream,
+  return mt_device_run(name, mt_state, mt_index, n_elem, threshold - 1, scratch, scratch_bytes, stream, threshold - 1,
                        [&](GenArgs& ga, hipStream_t s) {
                          ga.secrets = secrets;
                          ga.shares = static_cast<uint8_t*>(shares);

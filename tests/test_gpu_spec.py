@@ -50,9 +50,11 @@ def valid_limbs(block: torch.Tensor, n: int) -> np.ndarray:
     return np.stack([field.vec_to_limbs(h[r], n) for r in range(h.shape[0])])
 
 
-# the product library speculates on draws of at least 2^23 coefficients
-# (DN_MT_SPEC_MIN); smaller draws are tested through the tuning build with the
-# threshold at 0 (every draw with jump levels speculates)
+# the product library speculates after the generation on draws of at least
+# 2^23 coefficients (DN_MT_SPEC_MIN) and beside it from 2^16 where the levels
+# fit beside the generation (DN_MT_BESIDE_MIN); smaller draws are tested
+# through the tuning build with the thresholds at 0 (every draw with jump
+# levels speculates)
 SPEC_MIN = 1 << 23
 
 
@@ -81,6 +83,44 @@ def test_loop_of_equal_draws_hits_and_equals_host_draw(N, t, n, pre, monkeypatch
             _loop_case(N, t, n, pre)
     else:
         _loop_case(N, t, n, pre)
+
+
+@pytest.mark.parametrize("N,t,n,pre,lib", [((1 << 20) + 77, 3, 5, 333, "product"), (1 << 19, 5, 9, 0, "product"),
+                                           ((1 << 16) + 1, 3, 5, 5, "product"),
+                                           (40000, 3, 5, 17, "tuning"), (5000, 5, 9, 600, "tuning"),
+                                           ((1 << 21) + 9, 2, 3, 0, "tuning")])
+def test_loop_beside_a_small_generation(N, t, n, pre, lib, monkeypatch):
+    """Draws whose generation leaves a CU room for the jump levels' 83 KB
+    workgroups (at most ~1000 3-of-5 substreams, of 2^12 draws or at most
+    256 of 2^10) speculate beside the generation with those levels as they
+    are, from the next call's W_idx jumped on a side stream: the product
+    library from 2^16 coefficients (DN_MT_BESIDE_MIN; no speculation after the
+    generation below 2^23), the
+    tuning build with the threshold at 0 for the direct-level and radix-level
+    shapes below it.  Every call equals the host draw + split."""
+    if lib == "tuning":
+        monkeypatch.setenv("DN_MT_BESIDE_MIN", "0")
+        with _native.library(_native.TUNING_LIB):
+            _loop_case(N, t, n, pre)
+    else:
+        _loop_case(N, t, n, pre)
+
+
+def test_loop_of_coefficient_draws_beside(monkeypatch):
+    """The coefficient draw (dn_mt19937_draw_coeffs_device, one-register
+    rings) in a loop of equal draws of 2^20 + 5 elements x 2 coefficients:
+    speculated beside the generation, every draw equal to the host's."""
+    N, tm1 = (1 << 20) + 5, 2
+    a, b = random.Random(77), random.Random(77)
+    s0 = _native.mt_spec_stats()
+    out = torch.zeros((tm1, field.vec_bytes(N)), dtype=torch.uint8, device=dev())  # padding stays 0
+    for i in range(5):
+        assert _native.mt_draw_coeffs_device(a, N, tm1, out)
+        want = _native.mt_draw_coeffs(b, N, tm1)
+        assert np.array_equal(out.cpu().numpy(), want), i
+        assert a.getstate() == b.getstate(), i
+    d = delta(s0, _native.mt_spec_stats())
+    assert d["hits"] >= 3 and d["launched"] >= 4, d
 
 
 def _loop_case(N, t, n, pre):
