@@ -997,14 +997,14 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
         ss.random.seed(lg)
         sm = sec[:m]
         o2 = torch.empty((5, field.vec_bytes(m)), dtype=torch.uint8, device=dev)
-        for _ in range(2):
+        for _ in range(3):  # (the third call waits for the first speculation's side work)
             ss.make_shares_vec(sm, 5, out=o2)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(10):
+        for _ in range(20):
             ss.make_shares_vec(sm, 5, out=o2)
         torch.cuda.synchronize()
-        by_size[f"2^{lg}"] = (time.perf_counter() - t0) / 10 * 1e3
+        by_size[f"2^{lg}"] = (time.perf_counter() - t0) / 20 * 1e3
         del o2
     return {"workload": f"make_shares_vec(2^{log2n} int64, 5) on SecretShare(3), coefficients = the reference's "
                         "MT19937 draws (shamir.py:59-61), bit-exact", "unit": "elements/s",
@@ -1016,7 +1016,9 @@ def draw_split_row(dev, log2n: int, reps: int = 3) -> dict:
             "timing": "wall time per call; fused_ms: lone calls (a fresh SecretShare each: nothing to speculate "
                       f"on), the median over three output buffers of the best of {reps} calls on each (after >= "
                       "0.15 s of warm-up calls); loop_ms_per_call: back-to-back calls on one SecretShare, where "
-                      "each call's jump level was speculated by the call before (DN_MT_SPEC)",
+                      "each call's jump level was speculated by the call before (DN_MT_SPEC); fused_ms_by_size: "
+                      "20 back-to-back calls on one SecretShare per size after 3 (a loop, speculated from 2^16 "
+                      "coefficients where the levels fit beside the generation)",
             "equal_draw_then_split_and_state": ok, "fused_ms_by_size": by_size,
             "loop_ms_per_call": loop}
 
