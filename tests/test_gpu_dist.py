@@ -36,22 +36,47 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(world, N, t, n, mt_seed, sec_seed, tmp_path, backend="gloo"):
+def _start_ranks(world, args, backend, tmp_path, attempt):
     port = _free_port()
-    out = str(tmp_path / "res.json")
-    procs = []
+    procs, logs = [], []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), DN_DIST_BACKEND=backend)
-        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "gpu_dist_worker.py"), out,
-                                       str(N), str(t), str(n), str(mt_seed), str(sec_seed)], env=env))
-    try:
-        for p in procs:
-            p.wait(timeout=100)
-    finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
+        log = tmp_path / f"rank{r}.{attempt}.err"
+        logs.append(log)
+        with open(log, "w") as f:
+            procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "gpu_dist_worker.py"), *args],
+                                          env=env, stderr=f))
+    return procs, logs
+
+
+def run_ranks(world, N, t, n, mt_seed, sec_seed, tmp_path, backend="gloo"):
+    """The ranks as child processes on a free port; a start that lost the
+    port to another process (EADDRINUSE: the port is free when picked, not
+    reserved) is started again on a new one, at most three times."""
+    import time
+
+    out = str(tmp_path / "res.json")
+    args = [out, str(N), str(t), str(n), str(mt_seed), str(sec_seed)]
+    for attempt in range(3):
+        procs, logs = _start_ranks(world, args, backend, tmp_path, attempt)
+        lost_port = False
+        try:
+            deadline = time.monotonic() + 100
+            while any(p.poll() is None for p in procs) and time.monotonic() < deadline:
+                if any(p.poll() not in (None, 0) and "EADDRINUSE" in open(lg).read() for p, lg in zip(procs, logs)):
+                    lost_port = True
+                    break
+                time.sleep(0.2)
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+        if not lost_port:
+            break
+    for lg in logs:
+        sys.stderr.write(open(lg).read())
     assert [p.returncode for p in procs] == [0] * world
     res = []
     for r in range(world):
